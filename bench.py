@@ -1,0 +1,277 @@
+#!/usr/bin/env python3
+"""Benchmark of the KL screen hot path on MI355X (BASELINE.json metric).
+
+One step = one pass of the hot path over one batch of synthetic input, on
+every GPU: the batched KL fit of all of the rank's slots (``sf_kl_fit``)
+followed by the KL pixel evaluation of all of them (``sf_kl_eval``) into an
+HBM ring of output cubes.  Workload per GPU = BASELINE.json configs[2]
+(64 ant x 100 time x 16 freq x 20 dir, KL 256^2 screen); with --gpus N the
+antenna axis grows to 64 N and is sharded (weak scaling, configs[3] shape at
+N=4), with only one-shot setup collectives.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0.
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "ska-sdp-screen-fitting_amd"))
+
+METRIC = ("screen-slots/sec (ant×time×freq) + FITS-cube wall-clock, "
+          "KL 256² screen")
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+WORKLOADS = {
+    # name: (ant per GPU, times, freqs, dirs, grid side, cellsize)
+    "config3": (64, 100, 16, 20, 256, 0.01301),
+    "config2-shape": (62, 20, 12, 7, 128, 0.02602),
+    "config5-shape": (16, 50, 4, 50, 512, 0.006505),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="config3", choices=sorted(WORKLOADS))
+    ap.add_argument("--ring-gb", type=float, default=16.0,
+                    help="HBM ring for the output cubes (GiB)")
+    ap.add_argument("--fast-sincos", action="store_true",
+                    help="fp32 sincos epilogue after fp64 range reduction")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-workers", type=int, default=16)
+    ap.add_argument("--eval-only", action="store_true",
+                    help="time only sf_kl_eval (profiling)")
+    return ap.parse_args()
+
+
+# --------------------------------------------------------------------------
+# CPU baseline: the oracle (numpy fp64 restatement of the reference) on a
+# bounded slot sample, in a pool of single-threaded workers.
+# --------------------------------------------------------------------------
+def _cpu_worker(job):
+    os.environ["OMP_NUM_THREADS"] = "1"
+    sys.path.insert(0, REPO)
+    from oracle import kl as okl  # test infrastructure: baseline leg only
+
+    (phi, w, order, pp, cpix_args, n_eval) = job
+    basis = okl.Basis(pp)
+    t0 = time.perf_counter()
+    coefs = []
+    for k in range(phi.shape[0]):
+        white, _, _, _, _ = okl.fit_slot(phi[k], w[k], order[k], order[k], basis)
+        coefs.append(white)
+    t_fit = time.perf_counter() - t0
+    x, y = cpix_args
+    cpix = okl.cpix_matrix(pp, x, y)
+    t0 = time.perf_counter()
+    coefs = np.array(coefs)
+    for k in range(n_eval):
+        ph = okl.eval_phase_screens(coefs[k % len(coefs)][None, :], cpix)
+        planes = okl.eval_planes(ph).astype(np.float32)
+        del planes
+    t_eval = time.perf_counter() - t0
+    return phi.shape[0], t_fit, n_eval, t_eval
+
+
+def cpu_baseline(sol, setup, n_workers, slots_fit=64, slots_eval=192):
+    import multiprocessing as mp
+
+    T, F, A, D = sol.val.shape
+    ref = setup["ref_ant"]
+    phi = sol.val - setup["ref_phase"].cpu().numpy()[:, :, None, :]
+    jobs = []
+    rng = np.random.default_rng(1)
+    for k in range(n_workers):
+        a = [a for a in range(A) if a != ref][k % (A - 1)]
+        ts = rng.choice(T, size=min(slots_fit, T), replace=False)
+        f = k % F
+        jobs.append((phi[ts, f, a], sol.weight[ts, f, a],
+                     [setup["st_order"][a]] * len(ts), setup["piercepoints"],
+                     (setup["x"], setup["y"]), slots_eval))
+    ctx = mp.get_context("spawn")
+    t0 = time.perf_counter()
+    with ctx.Pool(n_workers) as pool:
+        res = pool.map(_cpu_worker, jobs)
+    wall = time.perf_counter() - t0
+    n_fit = sum(r[0] for r in res)
+    t_fit = sum(r[1] for r in res)
+    n_ev = sum(r[2] for r in res)
+    t_ev = sum(r[3] for r in res)
+    per_slot = t_fit / n_fit + t_ev / n_ev  # core-seconds per slot (fit + eval)
+    return {
+        "value": n_workers / per_slot,
+        "unit": "screen-slots/s",
+        "cores": n_workers,
+        "kind": "port",
+        "sample": (f"oracle (numpy fp64 restatement) on {n_fit} fit slots and "
+                   f"{n_ev} 256^2 eval slots of the same workload, "
+                   f"{n_workers} single-threaded workers, {wall:.1f} s wall; "
+                   f"fit {t_fit / n_fit * 1e3:.3f} ms/slot/core, eval "
+                   f"{t_ev / n_ev * 1e3:.1f} ms/slot/core"),
+    }
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from ska_sdp_screen_fitting_amd import get_context
+    from ska_sdp_screen_fitting_amd._lib import (SF_EVAL_FAST_SINCOS,
+                                                 SF_EVAL_NAN_SCRUB)
+    from ska_sdp_screen_fitting_amd.distributed import setup_shard
+    from ska_sdp_screen_fitting_amd.synthetic import (FIELD_DEC_DEG,
+                                                      FIELD_RA_DEG,
+                                                      FIELD_WIDTH_DEG,
+                                                      make_solutions)
+
+    A, T, F, D, N, cell = WORKLOADS[args.workload]
+    sol = make_solutions(n_ant=A, n_time=T, n_freq=F, n_dir=D,
+                         ant_offset=A * rank, n_ant_total=A * world)
+    setup = setup_shard(sol, A * rank, A * world, FIELD_RA_DEG, FIELD_DEC_DEG,
+                        FIELD_WIDTH_DEG, cell, device=dev if world > 1 else "cpu")
+    assert len(setup["x"]) == N
+
+    ctx = get_context(local_rank)
+    stream = torch.cuda.current_stream(dev)
+    ctx.set_stream(stream.cuda_stream)
+    ctx.set_basis(setup["piercepoints"], 100, 5.0 / 3.0)
+    ctx.set_grid(setup["x"], setup["y"])
+
+    S = T * F * A
+    P = N * N
+    phase = torch.from_numpy(sol.val).to(dev)
+    weight = torch.from_numpy(sol.weight).to(dev)
+    refph = setup["ref_phase"].to(dev).contiguous()
+    coef = torch.empty_like(phase)
+    resid = torch.empty_like(phase)
+    w_out = torch.empty_like(weight)
+    order_out = torch.empty((T, F, A), dtype=torch.int32, device=dev)
+    slot_bytes = 16 * P
+    ring = int(min(S, max(1, args.ring_gb * 2 ** 30 // slot_bytes)))
+    out = torch.empty((ring, 4, N, N), dtype=torch.float32, device=dev)
+    flags = SF_EVAL_NAN_SCRUB | (SF_EVAL_FAST_SINCOS if args.fast_sincos else 0)
+
+    def fit():
+        ctx.fit(phase, weight, T, F, A, setup["st_order"], niter=2,
+                nsigma=5.0, adjust_order=True, ref_ant=setup["ref_ant"],
+                coef=coef, resid=resid, w_out=w_out, order_out=order_out,
+                ant_offset=setup["ant_offset"], ref_phase=refph)
+
+    def evaluate():
+        ctx.eval(coef, S, out, ring, flags)
+
+    for _ in range(args.warmup):
+        if not args.eval_only:
+            fit()
+        evaluate()
+    if args.eval_only and args.warmup == 0:
+        fit()
+    torch.cuda.synchronize(dev)
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        if not args.eval_only:
+            fit()
+        ev[k][1].record(stream)
+        evaluate()
+        ev[k][2].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t_fit = float(np.mean([a.elapsed_time(b) for a, b, _ in ev])) * 1e-3
+    t_eval = float(np.mean([b.elapsed_time(c) for _, b, c in ev])) * 1e-3
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    elapsed = tmax.item()
+
+    # parity spot check (cheap invariants, not timed): |cos|^2 + |sin|^2 = 1
+    chk = out[: min(ring, 64)].float()
+    unit_err = float((chk[:, 0] ** 2 + chk[:, 1] ** 2 - 1).abs().max())
+
+    if rank == 0:
+        algo_bytes = S * (16 * P + 8 * D)
+        achieved = algo_bytes / t_eval / 1e9
+        traffic = None
+        tpath = os.path.join(REPO, "profiles", "traffic.json")
+        if os.path.exists(tpath):
+            try:
+                tj = json.load(open(tpath))
+                if tj.get("workload") == args.workload:
+                    traffic = tj.get("hbm_bytes_per_launch")
+            except (ValueError, OSError):
+                traffic = None
+        line = {
+            "metric": METRIC,
+            "value": S * world * args.steps / elapsed,
+            "unit": "screen-slots/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {
+                "workload": (f"{args.workload}: {A} ant x {T} time x {F} freq x "
+                             f"{D} dir per GPU (ant-sharded), KL {N}^2 screen, "
+                             "fit (phase, niter 2, adjust_order) + eval"),
+                "slots_per_gpu": S, "grid": N, "n_dir": D,
+                "parallelism": f"ant-shard x{world}",
+                "eval_sincos": "fp32-after-fp64-reduction" if args.fast_sincos else "fp64",
+                "eval_only": bool(args.eval_only),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel": "kl_eval_kernel",
+                "bytes_per_launch": algo_bytes,
+            },
+            "stages_ms": {"fit": t_fit * 1e3, "eval": t_eval * 1e3},
+            "check": {"max_abs_cos2_plus_sin2_minus_1": unit_err},
+        }
+        if not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(
+                sol, setup, max(1, min(args.cpu_workers, os.cpu_count() or 1)))
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,148 @@
+/*
+ * screenfit.h -- C ABI of the MI355X-native KL a-term screen library
+ * (libscreenfit.so, hand-written HIP for gfx950).
+ *
+ * Drop-in boundary for the hot path of ska-sdp-screen-fitting v0.1.0
+ * (reference at /root/reference, paths below relative to
+ * src/ska_sdp_screen_fitting/).  The reference is pure Python with no FFI;
+ * each entry point names the Python interface it replaces:
+ *
+ *   sf_set_basis  <- stationscreen._calculate_piercepoints / _calculate_svd
+ *                    (stationscreen.py:70-110, 390-430; run :1046-1053)
+ *   sf_kl_fit     <- stationscreen.run -> _process_single_freq ->
+ *                    _process_station -> _fit_screen
+ *                    (stationscreen.py:858-1161, 785-855, 597-782, 433-594)
+ *   sf_set_grid   <- KLScreen.make_matrix coordinate block
+ *                    (kl_screen.py:228-261)
+ *   sf_kl_eval    <- KLScreen.make_matrix + calculate_kl_screen + the NaN
+ *                    scrub of Screen.write (kl_screen.py:192-449,
+ *                    screen.py:343-378)
+ *
+ * Conventions
+ *  - Plain C types only.  Return 0 on success, a negative errno-style code
+ *    on failure (SF_EINVAL bad shape/argument, SF_ENOMEM, SF_EIO HIP
+ *    failure, SF_ENODEV no usable gfx950 device); sf_last_error() gives a
+ *    thread-local message.
+ *  - Array arguments of sf_kl_fit / sf_kl_eval are DEVICE pointers (HBM,
+ *    e.g. from sf_alloc or any HIP allocator); small geometry arrays
+ *    (piercepoints, grid coordinates, per-station orders) are HOST pointers.
+ *    The caller owns every buffer it passes; the library never frees caller
+ *    memory.  Device scratch (basis, pixel matrix) is owned by the context.
+ *  - Work is enqueued on the context's stream (sf_set_stream); calls return
+ *    once enqueued except sf_set_basis/sf_get_basis/sf_copy_* which
+ *    synchronise.  Calls on one context must be serialised by the caller;
+ *    contexts on different devices may be driven from different threads.
+ *  - Slot layout is the H5parm scalarphase layout [time][freq][ant][dir]
+ *    (stationscreen.py:936-963, kl_screen.py:269-272): slot index
+ *    s = (t * F + f) * A + a.  The evaluated cube is the FITS a-term cube
+ *    layout [time][freq][ant][4][y][x] (screen.py:319-351), native-endian
+ *    float32, planes (Re XX, Im XX, Re YY, Im YY).
+ */
+#ifndef SCREENFIT_H
+#define SCREENFIT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SF_OK 0
+#define SF_EINVAL (-22)
+#define SF_ENOMEM (-12)
+#define SF_EIO (-5)
+#define SF_ENODEV (-19)
+
+#define SF_MAX_DIR 60 /* directions per slot (one wavefront lane each; LDS-bound) */
+
+/* screen types of stationscreen.run (stationscreen.py:922-928) */
+#define SF_SCREEN_PHASE 0
+#define SF_SCREEN_TEC 1
+
+/* sf_kl_eval flags */
+#define SF_EVAL_NAN_SCRUB 1u /* NaN -> 1 (real planes), 0 (imag) (screen.py:368-378) */
+#define SF_EVAL_FAST_SINCOS (1u << 8) /* fp64 range reduction + fp32 sincos
+                                         (|err| <= 2e-7) instead of fp64 sincos */
+
+typedef struct sf_ctx sf_ctx;
+
+/* Operator parameters of stationscreen.run (stationscreen.py:858-871). */
+typedef struct sf_fit_params {
+  int screen_type;  /* SF_SCREEN_PHASE or SF_SCREEN_TEC */
+  int niter;        /* outlier-flagging iterations (phase: 2) */
+  double nsigma;    /* outlier threshold in circular sigmas (5.0) */
+  int adjust_order; /* adapt the order toward reduced chi^2 ~ 1 (1) */
+  int ref_ant;      /* GLOBAL reference station index, -1 = none */
+  int ant_offset;   /* global index of this call's station 0 (ant shards) */
+  const double* ref_phase; /* device [T][F][D] phases of the reference
+                              station when it is not in this shard; NULL =
+                              read them from station ref_ant - ant_offset */
+} sf_fit_params;
+
+/* Library / device management */
+const char* sf_version(void);
+const char* sf_last_error(void);
+int sf_create(int device, sf_ctx** out);
+int sf_destroy(sf_ctx* ctx);
+int sf_set_stream(sf_ctx* ctx, void* hip_stream); /* NULL = default stream */
+int sf_synchronize(sf_ctx* ctx);
+int sf_alloc(sf_ctx* ctx, size_t bytes, void** dev_ptr);
+int sf_free(sf_ctx* ctx, void* dev_ptr);
+int sf_copy_h2d(sf_ctx* ctx, void* dst_dev, const void* src_host, size_t bytes);
+int sf_copy_d2h(sf_ctx* ctx, void* dst_host, const void* src_dev, size_t bytes);
+
+/*
+ * Shared KL basis from the D piercepoints (host, [D][3] float64, the
+ * "piercepoint" array of the screen soltab): C[i][j] =
+ * -(|pp_i - pp_j|^2 / r0^2)^(beta/2) / 2, its pseudo-inverse with absolute
+ * cutoff 1e-3 (scipy>=1.7 pinv(rcond=1e-3) semantics) and U = the left
+ * singular vectors of C ordered by descending singular value.  Computed on
+ * the device (wavefront Jacobi eigen-solver).  1 <= D <= SF_MAX_DIR.
+ */
+int sf_set_basis(sf_ctx* ctx, const double* pp_host, int D, double r0,
+                 double beta);
+/* Copy the device basis back (host [D][D] each; any pointer may be NULL). */
+int sf_get_basis(sf_ctx* ctx, double* c_host, double* pinv_c_host,
+                 double* u_host, double* eig_host);
+
+/*
+ * Batched KL least-squares fit of all T*F*A slots (one scalar-phase or tec
+ * soltab, one pol).  Device inputs: phase [T][F][A][D] float64 (radians,
+ * NOT yet referenced -- the reference-station subtraction of
+ * stationscreen.py:994-997 is done here), weight [T][F][A][D] float32.
+ * Host input: station_order [A] (the initial per-station order,
+ * stationscreen.py:999-1034).  Device outputs (any may be NULL except
+ * coef): coef [T][F][A][D] float64 (the "phase_screen000" values),
+ * resid [T][F][A][D] float64, w_out [T][F][A][D] float32 (weights after
+ * outlier flagging), order_out [T][F][A] int32 (orders, the weights of the
+ * "...resid" soltab).  Requires sf_set_basis with the same D.
+ */
+int sf_kl_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,
+              int F, int A, const int* station_order_host,
+              const sf_fit_params* params, double* coef, double* resid,
+              float* w_out, int32_t* order_out);
+
+/*
+ * Pixel grid of the a-term image: X[nx], Y[ny] screen coordinates of the
+ * diagonal pixels (kl_screen.py:247-259, quirk Q8: pixel (y=j, x=i) is
+ * evaluated at (X[i], Y[j])).  Builds the [nx*ny][D] pixel basis on the
+ * device in MFMA fragment order.  Requires sf_set_basis first.
+ */
+int sf_set_grid(sf_ctx* ctx, const double* x_host, int nx,
+                const double* y_host, int ny);
+
+/*
+ * KL pixel evaluation of S slots: phase[s][p] = sum_d Cpix[p][d]*coef[s][d]
+ * (float64, MFMA), written as the 4 Jones planes (cos, sin, cos, sin) in
+ * float32 to out[(s % ring_slots)][4][ny][nx] (device).  ring_slots >= S
+ * writes every slot to its own place; smaller rings let a benchmark stream
+ * an output volume larger than HBM.  coef: device [S][D] float64.
+ */
+int sf_kl_eval(sf_ctx* ctx, const double* coef, int64_t S, float* out,
+               int64_t ring_slots, unsigned flags);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SCREENFIT_H */

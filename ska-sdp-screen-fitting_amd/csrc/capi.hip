@@ -1,0 +1,269 @@
+// capi.hip -- the extern "C" boundary of libscreenfit (include/screenfit.h).
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "sf_internal.h"
+
+namespace sf {
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+}  // namespace sf
+
+using sf::set_error;
+
+namespace {
+
+int check_device(int device) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0) {
+    set_error("no HIP device available");
+    return SF_ENODEV;
+  }
+  if (device < 0 || device >= n) {
+    set_error("device index out of range");
+    return SF_EINVAL;
+  }
+  hipDeviceProp_t prop;
+  SF_HIP(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    set_error(std::string("libscreenfit is built for gfx950, found ") +
+              prop.gcnArchName);
+    return SF_ENODEV;
+  }
+  return SF_OK;
+}
+
+template <typename T>
+int dev_alloc(T** p, size_t count) {
+  if (*p) {
+    hipFree(*p);
+    *p = nullptr;
+  }
+  if (count == 0) return SF_OK;
+  if (hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T)) != hipSuccess) {
+    *p = nullptr;
+    set_error("hipMalloc failed");
+    return SF_ENOMEM;
+  }
+  return SF_OK;
+}
+
+#define SF_TRY(x)              \
+  do {                         \
+    int rc_ = (x);             \
+    if (rc_ != SF_OK) return rc_; \
+  } while (0)
+
+}  // namespace
+
+extern "C" {
+
+const char* sf_version(void) { return "screenfit 0.1.0 (gfx950)"; }
+
+const char* sf_last_error(void) { return sf::g_last_error.c_str(); }
+
+int sf_create(int device, sf_ctx** out) {
+  SF_REQUIRE(out != nullptr, SF_EINVAL, "sf_create: out is NULL");
+  SF_TRY(check_device(device));
+  SF_HIP(hipSetDevice(device));
+  sf_ctx* ctx = new sf_ctx();
+  ctx->device = device;
+  *out = ctx;
+  return SF_OK;
+}
+
+int sf_destroy(sf_ctx* ctx) {
+  if (!ctx) return SF_OK;
+  hipSetDevice(ctx->device);
+  hipFree(ctx->d_pp);
+  hipFree(ctx->d_c);
+  hipFree(ctx->d_pinv);
+  hipFree(ctx->d_u);
+  hipFree(ctx->d_eig);
+  hipFree(ctx->d_cfrag);
+  hipFree(ctx->d_skip);
+  hipFree(ctx->d_st_order);
+  delete ctx;
+  return SF_OK;
+}
+
+int sf_set_stream(sf_ctx* ctx, void* stream) {
+  SF_REQUIRE(ctx, SF_EINVAL, "sf_set_stream: NULL context");
+  ctx->stream = reinterpret_cast<hipStream_t>(stream);
+  return SF_OK;
+}
+
+int sf_synchronize(sf_ctx* ctx) {
+  SF_REQUIRE(ctx, SF_EINVAL, "sf_synchronize: NULL context");
+  SF_HIP(hipSetDevice(ctx->device));
+  SF_HIP(hipStreamSynchronize(ctx->stream));
+  return SF_OK;
+}
+
+int sf_alloc(sf_ctx* ctx, size_t bytes, void** p) {
+  SF_REQUIRE(ctx && p, SF_EINVAL, "sf_alloc: bad argument");
+  SF_HIP(hipSetDevice(ctx->device));
+  if (hipMalloc(p, bytes) != hipSuccess) {
+    set_error("sf_alloc: hipMalloc failed");
+    return SF_ENOMEM;
+  }
+  return SF_OK;
+}
+
+int sf_free(sf_ctx* ctx, void* p) {
+  SF_REQUIRE(ctx, SF_EINVAL, "sf_free: NULL context");
+  SF_HIP(hipSetDevice(ctx->device));
+  SF_HIP(hipFree(p));
+  return SF_OK;
+}
+
+int sf_copy_h2d(sf_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  SF_REQUIRE(ctx && (bytes == 0 || (dst && src)), SF_EINVAL,
+             "sf_copy_h2d: bad argument");
+  SF_HIP(hipSetDevice(ctx->device));
+  SF_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  SF_HIP(hipStreamSynchronize(ctx->stream));
+  return SF_OK;
+}
+
+int sf_copy_d2h(sf_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  SF_REQUIRE(ctx && (bytes == 0 || (dst && src)), SF_EINVAL,
+             "sf_copy_d2h: bad argument");
+  SF_HIP(hipSetDevice(ctx->device));
+  SF_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  SF_HIP(hipStreamSynchronize(ctx->stream));
+  return SF_OK;
+}
+
+int sf_set_basis(sf_ctx* ctx, const double* pp, int D, double r0,
+                 double beta) {
+  SF_REQUIRE(ctx && pp, SF_EINVAL, "sf_set_basis: bad argument");
+  SF_REQUIRE(D >= 1 && D <= SF_MAX_DIR, SF_EINVAL,
+             "sf_set_basis: D out of range [1, SF_MAX_DIR]");
+  SF_REQUIRE(r0 > 0.0, SF_EINVAL, "sf_set_basis: r0 must be > 0");
+  SF_HIP(hipSetDevice(ctx->device));
+  SF_HIP(hipStreamSynchronize(ctx->stream));
+  SF_TRY(dev_alloc(&ctx->d_pp, (size_t)3 * D));
+  SF_TRY(dev_alloc(&ctx->d_c, (size_t)D * D));
+  SF_TRY(dev_alloc(&ctx->d_pinv, (size_t)D * D));
+  SF_TRY(dev_alloc(&ctx->d_u, (size_t)D * D));
+  SF_TRY(dev_alloc(&ctx->d_eig, (size_t)64));
+  SF_HIP(hipMemcpy(ctx->d_pp, pp, sizeof(double) * 3 * D,
+                   hipMemcpyHostToDevice));
+  SF_HIP(hipMemset(ctx->d_eig, 0, 64 * sizeof(double)));
+  ctx->D = D;
+  ctx->r0 = r0;
+  ctx->beta = beta;
+  // the grid (if any) belongs to the previous basis
+  ctx->nx = ctx->ny = 0;
+  ctx->n_pix = 0;
+  SF_TRY(sf::launch_basis(ctx));
+  SF_HIP(hipStreamSynchronize(ctx->stream));
+  return SF_OK;
+}
+
+int sf_get_basis(sf_ctx* ctx, double* c, double* pinv, double* u,
+                 double* eig) {
+  SF_REQUIRE(ctx && ctx->D > 0, SF_EINVAL, "sf_get_basis: no basis set");
+  SF_HIP(hipSetDevice(ctx->device));
+  SF_HIP(hipStreamSynchronize(ctx->stream));
+  const size_t n = (size_t)ctx->D * ctx->D * sizeof(double);
+  if (c) SF_HIP(hipMemcpy(c, ctx->d_c, n, hipMemcpyDeviceToHost));
+  if (pinv) SF_HIP(hipMemcpy(pinv, ctx->d_pinv, n, hipMemcpyDeviceToHost));
+  if (u) SF_HIP(hipMemcpy(u, ctx->d_u, n, hipMemcpyDeviceToHost));
+  if (eig)
+    SF_HIP(hipMemcpy(eig, ctx->d_eig, ctx->D * sizeof(double),
+                     hipMemcpyDeviceToHost));
+  return SF_OK;
+}
+
+int sf_kl_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,
+              int F, int A, const int* st_order, const sf_fit_params* p,
+              double* coef, double* resid, float* w_out, int32_t* order_out) {
+  SF_REQUIRE(ctx && ctx->D > 0, SF_EINVAL, "sf_kl_fit: call sf_set_basis first");
+  SF_REQUIRE(phase && weight && st_order && p && coef, SF_EINVAL,
+             "sf_kl_fit: NULL argument");
+  SF_REQUIRE(T >= 1 && F >= 1 && A >= 1, SF_EINVAL,
+             "sf_kl_fit: T, F, A must be >= 1");
+  SF_REQUIRE((int64_t)F * A <= INT32_MAX / 2, SF_EINVAL,
+             "sf_kl_fit: F * A too large");
+  SF_REQUIRE(p->screen_type == SF_SCREEN_PHASE || p->screen_type == SF_SCREEN_TEC,
+             SF_EINVAL, "sf_kl_fit: unsupported screen type");
+  SF_REQUIRE(p->niter >= 1, SF_EINVAL, "sf_kl_fit: niter must be >= 1");
+  SF_REQUIRE(p->screen_type == SF_SCREEN_PHASE || p->niter == 1, SF_EINVAL,
+             "sf_kl_fit: tec outlier iterations couple slots of a station "
+             "block and are not supported (use niter = 1)");
+  SF_REQUIRE(p->ref_ant >= -1 && p->ant_offset >= 0, SF_EINVAL,
+             "sf_kl_fit: bad ref_ant / ant_offset");
+  {
+    const int rl = p->ref_ant - p->ant_offset;
+    SF_REQUIRE(p->ref_ant == -1 || p->ref_phase || (rl >= 0 && rl < A),
+               SF_EINVAL,
+               "sf_kl_fit: reference station not in this shard and no "
+               "ref_phase given");
+  }
+  for (int a = 0; a < A; ++a)
+    SF_REQUIRE(st_order[a] >= 0, SF_EINVAL, "sf_kl_fit: negative order");
+  SF_HIP(hipSetDevice(ctx->device));
+  if (ctx->skip_cap < (size_t)F * A) {
+    SF_TRY(dev_alloc(&ctx->d_skip, (size_t)F * A));
+    ctx->skip_cap = (size_t)F * A;
+  }
+  if (ctx->st_order_cap < (size_t)A) {
+    SF_TRY(dev_alloc(&ctx->d_st_order, (size_t)A));
+    ctx->st_order_cap = (size_t)A;
+  }
+  SF_HIP(hipMemcpyAsync(ctx->d_st_order, st_order, sizeof(int) * A,
+                        hipMemcpyHostToDevice, ctx->stream));
+  return sf::launch_fit(ctx, phase, weight, T, F, A, p, coef, resid, w_out,
+                        order_out);
+}
+
+int sf_set_grid(sf_ctx* ctx, const double* x, int nx, const double* y,
+                int ny) {
+  SF_REQUIRE(ctx && ctx->D > 0, SF_EINVAL, "sf_set_grid: call sf_set_basis first");
+  SF_REQUIRE(x && y && nx >= 1 && ny >= 1, SF_EINVAL, "sf_set_grid: bad grid");
+  SF_REQUIRE((int64_t)nx * ny <= ((int64_t)1 << 31), SF_EINVAL,
+             "sf_set_grid: grid too large");
+  SF_HIP(hipSetDevice(ctx->device));
+  ctx->nx = nx;
+  ctx->ny = ny;
+  ctx->n_pix = (int64_t)nx * ny;
+  ctx->n_pix_blocks = (ctx->n_pix + sf::kBlockPix - 1) / sf::kBlockPix;
+  ctx->ksteps = (ctx->D + 3) / 4;
+  const size_t n = (size_t)ctx->n_pix_blocks * sf::kEvalWaves * ctx->ksteps *
+                   sf::kTiles * 64;
+  SF_TRY(dev_alloc(&ctx->d_cfrag, n));
+  double* dx = nullptr;
+  double* dy = nullptr;
+  SF_TRY(dev_alloc(&dx, (size_t)nx));
+  int rc = dev_alloc(&dy, (size_t)ny);
+  if (rc != SF_OK) {
+    hipFree(dx);
+    return rc;
+  }
+  hipMemcpyAsync(dx, x, sizeof(double) * nx, hipMemcpyHostToDevice, ctx->stream);
+  hipMemcpyAsync(dy, y, sizeof(double) * ny, hipMemcpyHostToDevice, ctx->stream);
+  rc = sf::launch_cpix(ctx, dx, dy);
+  hipStreamSynchronize(ctx->stream);
+  hipFree(dx);
+  hipFree(dy);
+  return rc;
+}
+
+int sf_kl_eval(sf_ctx* ctx, const double* coef, int64_t S, float* out,
+               int64_t ring, unsigned flags) {
+  SF_REQUIRE(ctx && ctx->n_pix > 0 && ctx->d_cfrag, SF_EINVAL,
+             "sf_kl_eval: call sf_set_grid first");
+  SF_REQUIRE(coef && out && S >= 0 && ring >= 1, SF_EINVAL,
+             "sf_kl_eval: bad argument");
+  if (S == 0) return SF_OK;
+  SF_HIP(hipSetDevice(ctx->device));
+  return sf::launch_eval(ctx, coef, S, out, ring, flags);
+}
+
+}  // extern "C"

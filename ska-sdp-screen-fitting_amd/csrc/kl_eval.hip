@@ -1,0 +1,232 @@
+// kl_eval.hip -- KL screen -> pixel-grid evaluation on gfx950.
+//
+// Replaces KLScreen.make_matrix + calculate_kl_screen (kl_screen.py:192-449):
+// for every slot s and pixel p
+//     phase[s][p] = sum_d Cpix[p][d] * coef[s][d]          (float64)
+//     out[s][0|2][p] = cos(phase), out[s][1|3][p] = sin(phase)  (float32)
+// Cpix is the same for every slot (kl_screen.py:446-448 depends only on the
+// piercepoints, r0, beta and the pixel coordinates), so the evaluation is one
+// dense (S x D) x (D x P) contraction followed by an elementwise epilogue --
+// HBM-write-bound (16 B written per pixel per slot).
+//
+// Mapping (one 64-lane wave):
+//   * v_mfma_f64_16x16x4_f64 with A = coef (16 slots x 4 dirs) and B = Cpix^T
+//     (4 dirs x 16 pixels); kTiles = 4 B tiles whose columns interleave so
+//     that lane l owns the 4 CONSECUTIVE pixels 4*(l&15) + t of a 64-pixel
+//     run -> every store is a 16-B float4, 16 lanes cover 256 contiguous B.
+//   * the wave keeps its Cpix fragments (ksteps x 4 doubles) in registers for
+//     its whole lifetime and streams slot groups of 16 through the MFMA.
+//   * the MFMA pipe does the contraction while the VALU does the sincos
+//     epilogue of the previous tile (independent waves on the SIMD).
+//   * block index -> (pixel block, slot chunk) is XCD-aware: the 8 XCDs each
+//     own 1/8 of the pixel blocks, so their Cpix slices stay in their L2.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "sf_internal.h"
+
+namespace sf {
+
+typedef double v4d __attribute__((ext_vector_type(4)));
+
+
+// f64 16x16x4 accumulator layout on gfx950: lane l, register r holds
+// D[row = (l >> 4) + 4 r][col = l & 15] (cdna_hip_programming.md §3).
+__device__ __forceinline__ int acc_row(int l, int r) { return (l >> 4) + 4 * r; }
+
+__device__ inline double pix_cov(double ppx, double ppy, double ppz, double x,
+                                 double y, double r0sq, double half_beta) {
+#pragma clang fp contract(off)
+  // numpy: sum(square(PIERCEPOINTS - (x, y, 0)), axis=1) -> ((.)+(.))+(.)
+  const double dx = ppx - x;
+  const double dy = ppy - y;
+  const double dz = ppz - 0.0;
+  const double d2 = (dx * dx + dy * dy) + dz * dz;
+  return -pow(d2 / r0sq, half_beta) / 2.0;
+}
+
+// Cpix in MFMA B-fragment order: [wave pixel block][kstep][tile][lane].
+__global__ __launch_bounds__(256) void kl_cpix_kernel(
+    const double* __restrict__ pp, int D, double r0, double beta,
+    const double* __restrict__ xs, int nx, const double* __restrict__ ys,
+    int ny, int ksteps, int64_t n_elems, double* __restrict__ cfrag) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n_elems) return;
+  const int l = (int)(e & 63);
+  const int t = (int)((e >> 6) % kTiles);
+  const int64_t rest = (e >> 6) / kTiles;
+  const int kk = (int)(rest % ksteps);
+  const int64_t wpb = rest / ksteps;
+  const int64_t p = wpb * kWavePix + (int64_t)(l & 15) * kTiles + t;
+  const int d = 4 * kk + (l >> 4);
+  double v = 0.0;
+  if (p < (int64_t)nx * ny && d < D) {
+    const int i = (int)(p % nx), j = (int)(p / nx);
+    v = pix_cov(pp[3 * d], pp[3 * d + 1], pp[3 * d + 2], xs[i], ys[j],
+                r0 * r0, beta / 2.0);
+  }
+  cfrag[e] = v;
+}
+
+__device__ __forceinline__ void jones_sincos(double ph, bool fast, float& s,
+                                             float& c) {
+  if (fast) {
+    // exact-ish fp64 reduction to [-pi, pi], then fp32 sincos
+    const double k = rint(ph * 0.15915494309189535);
+    double r = fma(-k, 6.283185307179586, ph);
+    r = fma(-k, 2.4492935982947064e-16, r);
+    sincosf((float)r, &s, &c);
+  } else {
+    double sd, cd;
+    sincos(ph, &sd, &cd);
+    s = (float)sd;
+    c = (float)cd;
+  }
+}
+
+template <int KS, bool VEC4>
+__global__ __launch_bounds__(256) void kl_eval_kernel(
+    const double* __restrict__ cfrag, const double* __restrict__ coef, int D,
+    int64_t S, int64_t P, int64_t n_pb, int64_t n_sc, int chunk_groups,
+    float* __restrict__ out, int64_t ring, unsigned flags, int fast) {
+  const int l = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  // XCD-aware block -> (pixel block, slot chunk)
+  const int64_t b = blockIdx.x;
+  int64_t pb, sc;
+  if ((n_pb & 7) == 0) {
+    const int64_t per = n_pb >> 3;
+    const int64_t x = b & 7, i = b >> 3;
+    pb = x * per + (i % per);
+    sc = i / per;
+  } else {
+    pb = b % n_pb;
+    sc = b / n_pb;
+  }
+  if (sc >= n_sc) return;
+  const int64_t wpb = pb * kEvalWaves + w;
+  const int64_t p0 = wpb * kWavePix + (int64_t)(l & 15) * kTiles;
+  if (wpb * kWavePix >= P) return;
+
+  double bf[KS][kTiles];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+    for (int t = 0; t < kTiles; ++t)
+      bf[kk][t] = cfrag[((wpb * KS + kk) * kTiles + t) * 64 + l];
+
+  const bool scrub = flags & SF_EVAL_NAN_SCRUB;
+  const bool fst = fast != 0;
+  const int64_t slot_base = sc * (int64_t)chunk_groups * 16;
+  for (int g = 0; g < chunk_groups; ++g) {
+    const int64_t s0 = slot_base + (int64_t)g * 16;
+    if (s0 >= S) break;
+    double af[KS];
+    {
+      const int64_t s = s0 + (l & 15);
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) {
+        const int d = 4 * kk + (l >> 4);
+        af[kk] = (s < S && d < D) ? coef[s * D + d] : 0.0;
+      }
+    }
+    v4d acc[kTiles];
+#pragma unroll
+    for (int t = 0; t < kTiles; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+      for (int t = 0; t < kTiles; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[kk], bf[kk][t],
+                                                      acc[t], 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t s = s0 + acc_row(l, r);
+      if (s >= S) continue;
+      float cv[kTiles], sv[kTiles];
+#pragma unroll
+      for (int t = 0; t < kTiles; ++t) {
+        jones_sincos(acc[t][r], fst, sv[t], cv[t]);
+        if (scrub) {
+          if (isnan(cv[t])) cv[t] = 1.0f;
+          if (isnan(sv[t])) sv[t] = 0.0f;
+        }
+      }
+      float* o = out + ((s % ring) * 4) * P + p0;
+      if (VEC4) {
+        const float4 c4 = make_float4(cv[0], cv[1], cv[2], cv[3]);
+        const float4 s4 = make_float4(sv[0], sv[1], sv[2], sv[3]);
+        *reinterpret_cast<float4*>(o) = c4;
+        *reinterpret_cast<float4*>(o + P) = s4;
+        *reinterpret_cast<float4*>(o + 2 * P) = c4;
+        *reinterpret_cast<float4*>(o + 3 * P) = s4;
+      } else {
+#pragma unroll
+        for (int t = 0; t < kTiles; ++t) {
+          if (p0 + t < P) {
+            o[t] = cv[t];
+            o[P + t] = sv[t];
+            o[2 * P + t] = cv[t];
+            o[3 * P + t] = sv[t];
+          }
+        }
+      }
+    }
+  }
+}
+
+int launch_cpix(sf_ctx* ctx, const double* d_x, const double* d_y) {
+  const int64_t n_wpb = ctx->n_pix_blocks * kEvalWaves;
+  const int64_t n = n_wpb * ctx->ksteps * kTiles * 64;
+  const int64_t blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(kl_cpix_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                     ctx->stream, ctx->d_pp, ctx->D, ctx->r0, ctx->beta, d_x,
+                     ctx->nx, d_y, ctx->ny, ctx->ksteps, n, ctx->d_cfrag);
+  SF_HIP(hipGetLastError());
+  return SF_OK;
+}
+
+template <int KS>
+static int launch_eval_ks(sf_ctx* ctx, const double* coef, int64_t S,
+                          float* out, int64_t ring, unsigned flags) {
+  const int64_t P = ctx->n_pix;
+  const int64_t n_pb = ctx->n_pix_blocks;
+  // slot chunk per workgroup: 16 groups of 16 slots (1 MiB of output at
+  // 256 pixels), fewer when S is small so the grid still fills 256 CUs
+  int groups = 16;
+  while (groups > 1 && n_pb * ((S + 16 * groups - 1) / (16 * groups)) < 2048)
+    groups >>= 1;
+  const int64_t n_sc = (S + 16 * groups - 1) / (16 * groups);
+  int64_t nblk = n_pb * n_sc;
+  if ((n_pb & 7) == 0) nblk = ((nblk + 7) / 8) * 8;
+  const bool vec4 = (P % 4 == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
+  const int fast = (flags >> 8) & 1;
+  if (vec4)
+    hipLaunchKernelGGL((kl_eval_kernel<KS, true>), dim3((unsigned)nblk),
+                       dim3(256), 0, ctx->stream, ctx->d_cfrag, coef, ctx->D,
+                       S, P, n_pb, n_sc, groups, out, ring, flags, fast);
+  else
+    hipLaunchKernelGGL((kl_eval_kernel<KS, false>), dim3((unsigned)nblk),
+                       dim3(256), 0, ctx->stream, ctx->d_cfrag, coef, ctx->D,
+                       S, P, n_pb, n_sc, groups, out, ring, flags, fast);
+  SF_HIP(hipGetLastError());
+  return SF_OK;
+}
+
+int launch_eval(sf_ctx* ctx, const double* coef, int64_t S, float* out,
+                int64_t ring, unsigned flags) {
+  switch (ctx->ksteps) {
+#define SF_KS(k) \
+  case k:        \
+    return launch_eval_ks<k>(ctx, coef, S, out, ring, flags);
+    SF_KS(1) SF_KS(2) SF_KS(3) SF_KS(4) SF_KS(5) SF_KS(6) SF_KS(7) SF_KS(8)
+    SF_KS(9) SF_KS(10) SF_KS(11) SF_KS(12) SF_KS(13) SF_KS(14) SF_KS(15)
+#undef SF_KS
+    default:
+      set_error("sf_kl_eval: unsupported number of directions");
+      return SF_EINVAL;
+  }
+}
+
+}  // namespace sf

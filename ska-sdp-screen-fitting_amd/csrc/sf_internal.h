@@ -1,0 +1,74 @@
+// sf_internal.h -- shared definitions of libscreenfit (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "screenfit.h"
+
+namespace sf {
+
+// error plumbing -------------------------------------------------------------
+void set_error(const std::string& msg);
+
+#define SF_HIP(call)                                                        \
+  do {                                                                      \
+    hipError_t e_ = (call);                                                 \
+    if (e_ != hipSuccess) {                                                 \
+      ::sf::set_error(std::string(#call) + ": " + hipGetErrorString(e_));   \
+      return SF_EIO;                                                        \
+    }                                                                       \
+  } while (0)
+
+#define SF_REQUIRE(cond, code, msg) \
+  do {                              \
+    if (!(cond)) {                  \
+      ::sf::set_error(msg);         \
+      return (code);                \
+    }                               \
+  } while (0)
+
+// pixel tiling of the evaluation kernel (kl_eval.hip) -------------------------
+constexpr int kTiles = 4;                       // 16x16 MFMA tiles per wave, interleaved
+constexpr int kWavePix = 16 * kTiles;           // 64 consecutive pixels per wave
+constexpr int kEvalWaves = 4;                   // waves per workgroup
+constexpr int kBlockPix = kWavePix * kEvalWaves; // 256 pixels per workgroup
+
+}  // namespace sf
+
+struct sf_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  // shared KL basis (sf_set_basis)
+  int D = 0;
+  double r0 = 100.0;
+  double beta = 5.0 / 3.0;
+  double* d_pp = nullptr;      // [D][3]
+  double* d_c = nullptr;       // [D][D]
+  double* d_pinv = nullptr;    // [D][D]
+  double* d_u = nullptr;       // [D][D] (columns sorted by |lambda| desc)
+  double* d_eig = nullptr;     // [D]    (signed eigenvalues, sorted)
+  // pixel grid (sf_set_grid)
+  int nx = 0, ny = 0;
+  int64_t n_pix = 0;
+  int64_t n_pix_blocks = 0;    // workgroup pixel blocks (kBlockPix)
+  int ksteps = 0;              // ceil(D / 4)
+  double* d_cfrag = nullptr;   // [wave pixel blocks][ksteps][kTiles][64]
+  // fit scratch
+  uint8_t* d_skip = nullptr;   // [F][A] block skip flags
+  size_t skip_cap = 0;
+  int* d_st_order = nullptr;   // [A]
+  size_t st_order_cap = 0;
+};
+
+namespace sf {
+int launch_basis(sf_ctx* ctx);
+int launch_cpix(sf_ctx* ctx, const double* d_x, const double* d_y);
+int launch_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,
+               int F, int A, const sf_fit_params* p, double* coef,
+               double* resid, float* w_out, int32_t* order_out);
+int launch_eval(sf_ctx* ctx, const double* coef, int64_t S, float* out,
+                int64_t ring, unsigned flags);
+}  // namespace sf

@@ -1,0 +1,194 @@
+"""ctypes binding of libscreenfit.so (the C ABI declared in include/screenfit.h).
+
+There is no fallback: if the library is missing or no gfx950 device is
+usable, every compute entry point raises :class:`ScreenFitError`.
+"""
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("SCREENFIT_LIB", os.path.join(_HERE, "libscreenfit.so"))
+
+SF_SCREEN_PHASE = 0
+SF_SCREEN_TEC = 1
+SF_EVAL_NAN_SCRUB = 1
+SF_EVAL_FAST_SINCOS = 1 << 8
+SF_MAX_DIR = 60
+
+# every symbol include/screenfit.h declares (checked by tests/test_capi.py)
+EXPORTED = (
+    "sf_version", "sf_last_error", "sf_create", "sf_destroy", "sf_set_stream",
+    "sf_synchronize", "sf_alloc", "sf_free", "sf_copy_h2d", "sf_copy_d2h",
+    "sf_set_basis", "sf_get_basis", "sf_kl_fit", "sf_set_grid", "sf_kl_eval",
+)
+
+
+class ScreenFitError(RuntimeError):
+    """Raised for any failure of the HIP library (including its absence)."""
+
+
+class FitParams(ctypes.Structure):
+    _fields_ = [("screen_type", ctypes.c_int), ("niter", ctypes.c_int),
+                ("nsigma", ctypes.c_double), ("adjust_order", ctypes.c_int),
+                ("ref_ant", ctypes.c_int), ("ant_offset", ctypes.c_int),
+                ("ref_phase", ctypes.c_void_p)]
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load_library(path=None):
+    """Load (once) and return the ctypes handle of libscreenfit.so."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise ScreenFitError(
+                f"libscreenfit.so not found at {p}: build it with "
+                "`make -C ska-sdp-screen-fitting_amd/csrc` (or "
+                "__graft_entry__.build()); there is no CPU fallback")
+        lib = ctypes.CDLL(p)
+        vp, ip, c_int, c_dbl = (ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+                                ctypes.c_int, ctypes.c_double)
+        i64 = ctypes.c_int64
+        sig = {
+            "sf_version": ([], ctypes.c_char_p),
+            "sf_last_error": ([], ctypes.c_char_p),
+            "sf_create": ([c_int, ctypes.POINTER(vp)], c_int),
+            "sf_destroy": ([vp], c_int),
+            "sf_set_stream": ([vp, vp], c_int),
+            "sf_synchronize": ([vp], c_int),
+            "sf_alloc": ([vp, ctypes.c_size_t, ctypes.POINTER(vp)], c_int),
+            "sf_free": ([vp, vp], c_int),
+            "sf_copy_h2d": ([vp, vp, vp, ctypes.c_size_t], c_int),
+            "sf_copy_d2h": ([vp, vp, vp, ctypes.c_size_t], c_int),
+            "sf_set_basis": ([vp, vp, c_int, c_dbl, c_dbl], c_int),
+            "sf_get_basis": ([vp, vp, vp, vp, vp], c_int),
+            "sf_kl_fit": ([vp, vp, vp, c_int, c_int, c_int, ip,
+                           ctypes.POINTER(FitParams), vp, vp, vp, vp], c_int),
+            "sf_set_grid": ([vp, vp, c_int, vp, c_int], c_int),
+            "sf_kl_eval": ([vp, vp, i64, vp, i64, ctypes.c_uint], c_int),
+        }
+        for name, (args, res) in sig.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = res
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def _check(rc, what):
+    if rc != 0:
+        msg = load_library().sf_last_error().decode(errors="replace")
+        raise ScreenFitError(f"{what} failed ({rc}): {msg}")
+
+
+def _ptr(x):
+    """Device/host pointer of a torch tensor, numpy array or int."""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if isinstance(x, np.ndarray):
+        assert x.flags["C_CONTIGUOUS"], "arrays passed to the C ABI must be contiguous"
+        return x.ctypes.data
+    if hasattr(x, "data_ptr"):
+        assert x.is_contiguous(), "tensors passed to the C ABI must be contiguous"
+        return x.data_ptr()
+    raise TypeError(type(x))
+
+
+class Context:
+    """One sf_ctx bound to one device.  Methods mirror the C ABI."""
+
+    def __init__(self, device=0):
+        self.lib = load_library()
+        self.device = device
+        h = ctypes.c_void_p()
+        _check(self.lib.sf_create(device, ctypes.byref(h)), "sf_create")
+        self.h = h
+        self.D = 0
+        self.grid = None
+
+    def close(self):
+        if self.h:
+            self.lib.sf_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_handle):
+        _check(self.lib.sf_set_stream(self.h, stream_handle), "sf_set_stream")
+
+    def synchronize(self):
+        _check(self.lib.sf_synchronize(self.h), "sf_synchronize")
+
+    def set_basis(self, pp, r0=100.0, beta=5.0 / 3.0):
+        pp = np.ascontiguousarray(pp, dtype=np.float64)
+        assert pp.ndim == 2 and pp.shape[1] == 3
+        _check(self.lib.sf_set_basis(self.h, pp.ctypes.data, pp.shape[0],
+                                     float(r0), float(beta)), "sf_set_basis")
+        self.D = pp.shape[0]
+        self.grid = None
+
+    def get_basis(self):
+        D = self.D
+        c, pinv, u = (np.empty((D, D)) for _ in range(3))
+        eig = np.empty(D)
+        _check(self.lib.sf_get_basis(self.h, c.ctypes.data, pinv.ctypes.data,
+                                     u.ctypes.data, eig.ctypes.data),
+               "sf_get_basis")
+        return c, pinv, u, eig
+
+    def fit(self, phase, weight, T, F, A, station_order, screen_type=0,
+            niter=2, nsigma=5.0, adjust_order=True, ref_ant=-1, coef=None,
+            resid=None, w_out=None, order_out=None, ant_offset=0,
+            ref_phase=None):
+        """sf_kl_fit on device buffers (torch tensors or raw pointers)."""
+        so = np.ascontiguousarray(station_order, dtype=np.int32)
+        assert so.shape == (A,)
+        prm = FitParams(int(screen_type), int(niter), float(nsigma),
+                        int(bool(adjust_order)), int(ref_ant), int(ant_offset),
+                        _ptr(ref_phase))
+        _check(self.lib.sf_kl_fit(
+            self.h, _ptr(phase), _ptr(weight), int(T), int(F), int(A),
+            so.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+            ctypes.byref(prm), _ptr(coef), _ptr(resid), _ptr(w_out),
+            _ptr(order_out)), "sf_kl_fit")
+
+    def set_grid(self, x, y):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        y = np.ascontiguousarray(y, dtype=np.float64)
+        _check(self.lib.sf_set_grid(self.h, x.ctypes.data, x.size,
+                                    y.ctypes.data, y.size), "sf_set_grid")
+        self.grid = (x.size, y.size)
+
+    def eval(self, coef, S, out, ring_slots=None, flags=SF_EVAL_NAN_SCRUB):
+        ring = int(S if ring_slots is None else ring_slots)
+        _check(self.lib.sf_kl_eval(self.h, _ptr(coef), int(S), _ptr(out),
+                                   max(ring, 1), int(flags)), "sf_kl_eval")
+
+
+_contexts = {}
+
+
+def get_context(device=0):
+    """Process-wide context per device (bound to torch's current stream by
+    the callers that use torch)."""
+    ctx = _contexts.get(device)
+    if ctx is None:
+        ctx = Context(device)
+        _contexts[device] = ctx
+    return ctx

@@ -1,0 +1,167 @@
+"""KL (Karhunen-Loeve) screens on the MI355X (kl_screen.py:22-449 of the
+reference).
+
+``KLScreen`` keeps the reference's constructor and methods.  ``fit`` runs the
+batched GPU fit (``stationscreen.run``); ``make_matrix`` and ``write``
+evaluate the screens with the HIP kernel ``kl_eval_kernel`` (MFMA float64
+contraction + sincos epilogue) instead of a per-pixel Python loop in a
+process pool.
+"""
+
+import multiprocessing
+
+import numpy as np
+
+from . import geometry
+from . import stationscreen
+from ._lib import SF_EVAL_NAN_SCRUB, get_context
+from .h5parm import H5parm, get_reference_station
+from .screen import Screen
+
+
+def read_patch_names(skymodel_filename):
+    """Patch names of a makesourcedb sky model (the patch lines ``, , name,
+    ra, dec``), i.e. the keys of lsmtool ``getPatchPositions()``."""
+    names = []
+    with open(skymodel_filename, encoding="utf8") as fh:
+        for line in fh:
+            parts = [p.strip() for p in line.split(",")]
+            if len(parts) >= 5 and parts[0] == "" and parts[1] == "" and parts[2]:
+                names.append(parts[2])
+    return names
+
+
+class KLEvaluator:
+    """Device state for evaluating KL screens on one grid."""
+
+    def __init__(self, piercepoints, r_0, beta, x_coord, y_coord, device=0):
+        import torch
+
+        self.torch = torch
+        self.dev = torch.device("cuda", device)
+        self.ctx = get_context(device)
+        self.pp = np.asarray(piercepoints, np.float64)
+        self.D = self.pp.shape[0]
+        self.nx, self.ny = len(x_coord), len(y_coord)
+        with torch.cuda.device(self.dev):
+            self.ctx.set_stream(torch.cuda.current_stream(self.dev).cuda_stream)
+            self.ctx.set_basis(self.pp, r_0, beta)
+            self.ctx.set_grid(x_coord, y_coord)
+
+    def eval_device(self, coef_dev, out_dev=None, flags=SF_EVAL_NAN_SCRUB):
+        """coef_dev: device [S, D] float64 -> device [S, 4, ny, nx] float32."""
+        torch = self.torch
+        S = coef_dev.shape[0]
+        if out_dev is None:
+            out_dev = torch.empty((S, 4, self.ny, self.nx), dtype=torch.float32,
+                                  device=self.dev)
+        with torch.cuda.device(self.dev):
+            self.ctx.set_stream(torch.cuda.current_stream(self.dev).cuda_stream)
+            self.ctx.eval(coef_dev, S, out_dev, S, flags)
+        return out_dev
+
+    def eval_host(self, coef, flags=SF_EVAL_NAN_SCRUB):
+        """coef: host [..., D] -> host float32 [..., 4, ny, nx]."""
+        coef = np.ascontiguousarray(coef, np.float64)
+        lead = coef.shape[:-1]
+        c = self.torch.from_numpy(coef.reshape(-1, self.D)).to(self.dev)
+        out = self.eval_device(c, flags=flags)
+        return out.cpu().numpy().reshape(lead + (4, self.ny, self.nx))
+
+
+class KLScreen(Screen):
+    """Class for KL (Karhunen-Lo`eve) screens (kl_screen.py:22)."""
+
+    def __init__(self, name, h5parm_filename, skymodel_filename, rad, dec,
+                 width_ra, width_dec, solset_name="sol000",
+                 phase_soltab_name="phase000", amplitude_soltab_name=None):
+        super().__init__(name, h5parm_filename, skymodel_filename, rad, dec,
+                         width_ra, width_dec, solset_name=solset_name,
+                         phase_soltab_name=phase_soltab_name,
+                         amplitude_soltab_name=amplitude_soltab_name)
+        self.height = None
+        self.beta_val = None
+        self.r_0 = None
+        self.piercepoints = None
+        self.mid_ra = None
+        self.mid_dec = None
+        self._evaluators = {}
+
+    def fit(self):
+        """Fit screens to the input solutions (kl_screen.py:61-155)."""
+        if not self.phase_only:
+            raise NotImplementedError(
+                "amplitude (gain) KL screens are the next row of the build")
+        h5 = H5parm(self.input_h5parm_filename)
+        solset = h5.get_solset(self.input_solset_name)
+        soltab_ph = solset.get_soltab(self.input_phase_soltab_name)
+        dirs = [str(d) for d in soltab_ph.dir]
+        if self.input_skymodel_filename is not None:
+            patches = set(read_patch_names(self.input_skymodel_filename))
+            missing = [d for d in dirs if d.strip("[]") not in patches]
+            if missing:  # the reference raises KeyError here (kl_screen.py:79)
+                raise KeyError(f"directions not in the sky model: {missing}")
+        ref_ind = get_reference_station(soltab_ph, 10)
+        screen_order = min(20, len(dirs) - 1)
+        stationscreen.run(soltab_ph, "phase_screen000", order=screen_order,
+                          ref_ant=ref_ind, scale_order=True, adjust_order=True,
+                          ncpu=self.ncpu or 0, device=self.device)
+        st = solset.get_soltab("phase_screen000")
+        self.vals_ph = st.val
+        self.times_ph = np.asarray(st.time)
+        self.freqs_ph = np.asarray(st.freq)
+        self.source_names = st.dir
+        self.source_dict = solset.get_source()
+        self.source_positions = [self.source_dict[s] for s in self.source_names]
+        self.station_names = st.ant
+        self.station_dict = solset.get_ant()
+        self.station_positions = [self.station_dict[s] for s in self.station_names]
+        self.height = st.attrs["height"]
+        self.beta_val = st.attrs["beta"]
+        self.r_0 = st.attrs["r_0"]
+        self.piercepoints = np.array(st.piercepoint)
+        self.mid_ra = st.attrs["midra"]
+        self.mid_dec = st.attrs["middec"]
+        h5.close()
+
+    def get_memory_usage(self, cellsize_deg):
+        """GB per time slot, the reference's estimate (kl_screen.py:157-190:
+        int() sizes, /10 overhead, x ncpu) so that time chunking matches."""
+        ncpu = self.ncpu or multiprocessing.cpu_count()
+        ximsize = int(self.width_ra / cellsize_deg)
+        yimsize = int(self.width_dec / cellsize_deg)
+        nbytes = 8 * len(self.freqs_ph) * len(self.station_names) * 4 * yimsize * ximsize
+        return nbytes / 1024 ** 3 / 10 * ncpu
+
+    def evaluator(self, cellsize_deg):
+        key = float(cellsize_deg)
+        ev = self._evaluators.get(key)
+        if ev is None:
+            x, y = geometry.grid_coords(self.rad, self.dec, self.width_ra,
+                                        cellsize_deg, self.mid_ra, self.mid_dec)
+            ev = KLEvaluator(self.piercepoints, self.r_0, self.beta_val, x, y,
+                             self.device)
+            self._evaluators = {key: ev}
+        return ev
+
+    def make_matrix(self, t_start_index, t_stop_index, freq_ind, stat_ind,
+                    cellsize_deg, out_dir, ncpu):
+        """(t_stop - t_start, 4, ny, nx) float64 (kl_screen.py:192-380); the
+        values carry the float32 rounding of the FITS cube (Q12)."""
+        del out_dir, ncpu
+        coef = np.asarray(self.vals_ph)[t_start_index:t_stop_index, freq_ind,
+                                        stat_ind, :]
+        return self.evaluator(cellsize_deg).eval_host(coef).astype(np.float64)
+
+    def write_chunk(self, writer, g_start, g_stop, cellsize_deg, smooth_pix,
+                    max_batch_bytes=2 << 30):
+        """All (freq, station) screens of times [g_start, g_stop) in device
+        batches of whole time rows, streamed to the FITS writer."""
+        ev = self.evaluator(cellsize_deg)
+        vals = np.asarray(self.vals_ph)
+        n_f, n_a = vals.shape[1], vals.shape[2]
+        row_bytes = n_f * n_a * 4 * ev.nx * ev.ny * 4
+        rows = max(1, int(max_batch_bytes // max(row_bytes, 1)))
+        for t0 in range(g_start, g_stop, rows):
+            t1 = min(g_stop, t0 + rows)
+            writer.write(ev.eval_host(vals[t0:t1]))
