@@ -46,8 +46,9 @@ def parse():
     ap.add_argument("--workload", default="config3", choices=sorted(WORKLOADS))
     ap.add_argument("--ring-gb", type=float, default=16.0,
                     help="HBM ring for the output cubes (GiB)")
-    ap.add_argument("--fast-sincos", action="store_true",
-                    help="fp32 sincos epilogue after fp64 range reduction")
+    ap.add_argument("--precise-sincos", action="store_true",
+                    help="fp64 sincos epilogue (default: fp64 range reduction "
+                         "+ fp32 sincos, |err| <= 3e-7)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-workers", type=int, default=16)
     ap.add_argument("--eval-only", action="store_true",
@@ -171,7 +172,7 @@ def main():
     slot_bytes = 16 * P
     ring = int(min(S, max(1, args.ring_gb * 2 ** 30 // slot_bytes)))
     out = torch.empty((ring, 4, N, N), dtype=torch.float32, device=dev)
-    flags = SF_EVAL_NAN_SCRUB | (SF_EVAL_FAST_SINCOS if args.fast_sincos else 0)
+    flags = SF_EVAL_NAN_SCRUB | (0 if args.precise_sincos else SF_EVAL_FAST_SINCOS)
 
     def fit():
         ctx.fit(phase, weight, T, F, A, setup["st_order"], niter=2,
@@ -207,6 +208,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    fit_stats = ctx.fit_stats() if not args.eval_only else {}
     t_fit = float(np.mean([a.elapsed_time(b) for a, b, _ in ev])) * 1e-3
     t_eval = float(np.mean([b.elapsed_time(c) for _, b, c in ev])) * 1e-3
     tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -249,7 +251,7 @@ def main():
                              "fit (phase, niter 2, adjust_order) + eval"),
                 "slots_per_gpu": S, "grid": N, "n_dir": D,
                 "parallelism": f"ant-shard x{world}",
-                "eval_sincos": "fp32-after-fp64-reduction" if args.fast_sincos else "fp64",
+                "eval_sincos": "fp64" if args.precise_sincos else "fp32-after-fp64-reduction",
                 "eval_only": bool(args.eval_only),
             },
             "roofline": {
@@ -263,6 +265,7 @@ def main():
                 "bytes_per_launch": algo_bytes,
             },
             "stages_ms": {"fit": t_fit * 1e3, "eval": t_eval * 1e3},
+            "fit_stats": fit_stats,
             "check": {"max_abs_cos2_plus_sin2_minus_1": unit_err},
         }
         if not args.no_cpu_baseline:

@@ -87,6 +87,11 @@ int sf_create(int device, sf_ctx** out);
 int sf_destroy(sf_ctx* ctx);
 int sf_set_stream(sf_ctx* ctx, void* hip_stream); /* NULL = default stream */
 int sf_synchronize(sf_ctx* ctx);
+/* Options: SF_OPT_FIT_GENERAL = 1 routes every slot through the general
+ * (per-slot Jacobi) fit kernel instead of the mask-cached eigenbasis
+ * pipeline; both give the reference's results (used to cross-check). */
+#define SF_OPT_FIT_GENERAL 1
+int sf_set_option(sf_ctx* ctx, int option, int value);
 int sf_alloc(sf_ctx* ctx, size_t bytes, void** dev_ptr);
 int sf_free(sf_ctx* ctx, void* dev_ptr);
 int sf_copy_h2d(sf_ctx* ctx, void* dst_dev, const void* src_host, size_t bytes);
@@ -122,6 +127,11 @@ int sf_kl_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,
               int F, int A, const int* station_order_host,
               const sf_fit_params* params, double* coef, double* resid,
               float* w_out, int32_t* order_out);
+
+/* Statistics of the last sf_kl_fit (synchronises): number of distinct
+ * flagged-direction masks whose subset basis was decomposed, and number of
+ * slots that took the general (tiny-weight) path. */
+int sf_get_fit_stats(sf_ctx* ctx, int* n_masks, int* n_general);
 
 /*
  * Pixel grid of the a-term image: X[nx], Y[ny] screen coordinates of the

@@ -87,6 +87,17 @@ int sf_destroy(sf_ctx* ctx) {
   hipFree(ctx->d_cfrag);
   hipFree(ctx->d_skip);
   hipFree(ctx->d_st_order);
+  hipFree(ctx->d_keys);
+  hipFree(ctx->d_ids);
+  hipFree(ctx->d_pool_mask);
+  hipFree(ctx->d_pool);
+  hipFree(ctx->d_pos);
+  hipFree(ctx->d_slow);
+  hipFree(ctx->d_class);
+  hipFree(ctx->d_counters);
+  hipFree(ctx->d_scratch);
+  hipFree(ctx->d_wscratch);
+  hipFree(ctx->d_oscratch);
   delete ctx;
   return SF_OK;
 }
@@ -95,6 +106,18 @@ int sf_set_stream(sf_ctx* ctx, void* stream) {
   SF_REQUIRE(ctx, SF_EINVAL, "sf_set_stream: NULL context");
   ctx->stream = reinterpret_cast<hipStream_t>(stream);
   return SF_OK;
+}
+
+int sf_set_option(sf_ctx* ctx, int option, int value) {
+  SF_REQUIRE(ctx, SF_EINVAL, "sf_set_option: NULL context");
+  switch (option) {
+    case SF_OPT_FIT_GENERAL:
+      ctx->force_general = value != 0;
+      return SF_OK;
+    default:
+      set_error("sf_set_option: unknown option");
+      return SF_EINVAL;
+  }
 }
 
 int sf_synchronize(sf_ctx* ctx) {
@@ -221,6 +244,18 @@ int sf_kl_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,
                         hipMemcpyHostToDevice, ctx->stream));
   return sf::launch_fit(ctx, phase, weight, T, F, A, p, coef, resid, w_out,
                         order_out);
+}
+
+int sf_get_fit_stats(sf_ctx* ctx, int* n_masks, int* n_general) {
+  SF_REQUIRE(ctx, SF_EINVAL, "sf_get_fit_stats: NULL context");
+  int c[4] = {0, 0, 0, 0};
+  SF_HIP(hipSetDevice(ctx->device));
+  SF_HIP(hipStreamSynchronize(ctx->stream));
+  if (ctx->d_counters)
+    SF_HIP(hipMemcpy(c, ctx->d_counters, sizeof(c), hipMemcpyDeviceToHost));
+  if (n_masks) *n_masks = c[0];
+  if (n_general) *n_general = c[2];
+  return SF_OK;
 }
 
 int sf_set_grid(sf_ctx* ctx, const double* x, int nx, const double* y,

@@ -384,7 +384,8 @@ __device__ void fit_screen(const FitLds& L, const SubsetState& st, int D,
   resid_d = phi_d - screen_all;
 }
 
-__global__ __launch_bounds__(256) void kl_fit_kernel(
+__global__ __launch_bounds__(256) void kl_fit_general_kernel(
+    const int* __restrict__ slot_list, const int* __restrict__ n_list,
     const double* __restrict__ phase, const float* __restrict__ weight,
     int T, int F, int A, int D, const int* __restrict__ st_order,
     const uint8_t* __restrict__ skip, const double* __restrict__ refph,
@@ -421,9 +422,12 @@ __global__ __launch_bounds__(256) void kl_fit_kernel(
   for (int e = threadIdx.x; e < D; e += blockDim.x) L.eig[e] = g_eig[e];
   __syncthreads();
 
-  const int64_t S = (int64_t)T * F * A;
-  for (int64_t s = (int64_t)blockIdx.x * nwaves + wv; s < S;
-       s += (int64_t)gridDim.x * nwaves) {
+  // either all slots or the slots of a device-side list (the slow path of
+  // kl_fit_fast.hip: tiny weights, mask-pool overflow)
+  const int64_t S = slot_list ? (int64_t)n_list[0] : (int64_t)T * F * A;
+  for (int64_t j = (int64_t)blockIdx.x * nwaves + wv; j < S;
+       j += (int64_t)gridDim.x * nwaves) {
+    const int64_t s = slot_list ? (int64_t)slot_list[j] : j;
     const int a = (int)(s % A);
     const int f = (int)((s / A) % F);
     const int64_t base = s * D;
@@ -557,49 +561,58 @@ int launch_basis(sf_ctx* ctx) {
   return SF_OK;
 }
 
-int launch_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,
-               int F, int A, const sf_fit_params* p, double* coef,
-               double* resid, float* w_out, int32_t* order_out) {
-  const int D = ctx->D;
-  // local index of the reference station (may be outside [0, A) when the
-  // station lives in another shard: then p->ref_phase carries its phases)
+// Referencing / ref-station skip parameters of one sf_kl_fit call
+// (stationscreen.py:994-997, :818), including the operator-precedence quirk
+// Q15 (tec is always referenced, to the last (local) station when
+// ref_ant == -1).
+RefSpec ref_spec(const sf_fit_params* p, int A) {
+  RefSpec r;
   const int ref = (p->ref_ant == -1) ? -1 : p->ref_ant - p->ant_offset;
-  const bool ref_local = ref >= 0 && ref < A;
-  // referencing and the ref-station skip (stationscreen.py:994-997, :818),
-  // including the operator-precedence quirk Q15 (tec is always referenced,
-  // to the last (local) station when ref_ant == -1)
-  int ref_sub = -1, ref_skip = -1;
-  const double* refph = nullptr;
   if (p->screen_type == SF_SCREEN_PHASE) {
     if (p->ref_ant != -1) {
-      if (p->ref_phase) refph = p->ref_phase; else ref_sub = ref;
+      if (p->ref_phase) r.refph = p->ref_phase; else r.sub = ref;
     }
   } else {
-    if (p->ref_ant == -1) ref_sub = A - 1;
-    else if (p->ref_phase) refph = p->ref_phase;
-    else ref_sub = ref;
+    if (p->ref_ant == -1) r.sub = A - 1;
+    else if (p->ref_phase) r.refph = p->ref_phase;
+    else r.sub = ref;
   }
-  if (ref_local) ref_skip = ref;
+  if (ref >= 0 && ref < A) r.skip = ref;
+  return r;
+}
+
+int launch_skip(sf_ctx* ctx, const double* phase, const float* weight, int T,
+                int F, int A, const RefSpec& r) {
   hipLaunchKernelGGL(kl_skip_kernel, dim3(F * A), dim3(64), 0, ctx->stream,
-                     phase, weight, T, F, A, D, ref_sub, refph, ctx->d_skip);
+                     phase, weight, T, F, A, ctx->D, r.sub, r.refph, ctx->d_skip);
   SF_HIP(hipGetLastError());
+  return SF_OK;
+}
+
+int launch_fit_general(sf_ctx* ctx, const int* slot_list, const int* n_list,
+                       int64_t max_slots, const double* phase,
+                       const float* weight, int T, int F, int A,
+                       const sf_fit_params* p, const RefSpec& r, double* coef,
+                       double* resid, float* w_out, int32_t* order_out) {
+  const int D = ctx->D;
   const size_t shared = fit_shared_bytes(D);
   const size_t wave = fit_wave_bytes(D);
   int nw = 4;
   while (nw > 1 && shared + nw * wave > 80 * 1024) --nw;
   const size_t shm = shared + nw * wave;
-  const int64_t S = (int64_t)T * F * A;
-  int64_t blocks = (S + nw - 1) / nw;
-  if (blocks > 8192) blocks = 8192;
+  int64_t blocks = (max_slots + nw - 1) / nw;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
   if (shm > 64 * 1024)
-    SF_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&kl_fit_kernel),
-                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)shm));
-  hipLaunchKernelGGL(kl_fit_kernel, dim3((unsigned)blocks), dim3(64 * nw), shm,
-                     ctx->stream, phase, weight, T, F, A, D, ctx->d_st_order,
-                     ctx->d_skip, refph, ctx->d_c, ctx->d_u, ctx->d_eig,
-                     p->screen_type, p->niter, p->nsigma, p->adjust_order,
-                     ref_sub, ref_skip, coef, resid, w_out, order_out);
+    SF_HIP(hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&kl_fit_general_kernel),
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+  hipLaunchKernelGGL(kl_fit_general_kernel, dim3((unsigned)blocks),
+                     dim3(64 * nw), shm, ctx->stream, slot_list, n_list, phase,
+                     weight, T, F, A, D, ctx->d_st_order, ctx->d_skip, r.refph,
+                     ctx->d_c, ctx->d_u, ctx->d_eig, p->screen_type, p->niter,
+                     p->nsigma, p->adjust_order, r.sub, r.skip, coef, resid,
+                     w_out, order_out);
   SF_HIP(hipGetLastError());
   return SF_OK;
 }

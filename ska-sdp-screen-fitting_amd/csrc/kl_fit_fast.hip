@@ -1,0 +1,753 @@
+// kl_fit_fast.hip -- the production KL fit pipeline (gfx950, float64).
+//
+// Same result as kl_fit_general_kernel (and the reference operator
+// stationscreen.run, stationscreen.py:597-782 / 433-594), restructured for
+// throughput:
+//
+//  1. flagged-direction subsets are decomposed ONCE PER UNIQUE FLAG MASK
+//     (the reference recomputes _calculate_svd for every slot with a flagged
+//     direction, stationscreen.py:495-499): a device hash table maps each
+//     64-bit unflagged-mask to an entry of a pool of subset bases (U_sub
+//     sorted by |lambda|, lambda), filled by a wavefront Jacobi kernel;
+//  2. the least-squares solve runs in the eigenbasis of C.  With
+//     C = U Lambda U^T, pinv(C) U_k = U_k Lambda_k^+ and C pinv(C) U_k =
+//     U_k (Lambda_k Lambda_k^+), so
+//        C re = U_k m(a_c),  a_c = (U_k^T W U_k)^+ U_k^T W cos(phi)
+//        white = U Lambda^+ U^T screen,  C white = U (Lambda Lambda^+) U^T screen
+//     (m = mask of |lambda| > 1e-3).  No C / pinv(C) mat-vecs remain, and for
+//     uniform unflagged weights (the common 0/1 case) U_k^T W U_k = w I;
+//  3. slots with a weight in (0, 1.001e-3] -- where the 1e-3 pinv cutoff on
+//     U_k^T W U_k can truncate -- are routed to kl_fit_general_kernel, which
+//     keeps the reference's exact pinv semantics through a Jacobi solve.
+//
+// The outlier-flagging iterations become passes over all slots; between
+// passes the new masks are inserted, numbered and decomposed.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdlib>
+
+#include "sf_internal.h"
+#include "sf_wave.h"
+
+namespace sf {
+
+constexpr double kAtol = 1e-3;             // pinv(rcond=1e-3)
+constexpr double kTinyW = 1e-3 * 1.001;    // slow-path threshold on weights
+constexpr unsigned long long kEmptyKey = 0ull;
+
+__host__ __device__ inline int ldo(int n) { return n | 1; }
+
+__device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
+  x ^= x >> 30;
+  x *= 0xbf58476d1ce4e5b9ull;
+  x ^= x >> 27;
+  x *= 0x94d049bb133111ebull;
+  x ^= x >> 31;
+  return x;
+}
+
+// Insert `key` (non-zero) into the open-addressing table; returns its slot
+// or -3 when the table is full.  Only ever inserts, never waits on other
+// threads (ids are assigned by a later kernel).
+__device__ int table_insert(unsigned long long* keys, int cap,
+                            unsigned long long key) {
+  int h = (int)(mix64(key) & (unsigned long long)(cap - 1));
+  for (int probe = 0; probe < cap; ++probe) {
+    const unsigned long long prev = atomicCAS(keys + h, kEmptyKey, key);
+    if (prev == kEmptyKey || prev == key) return h;
+    h = (h + 1) & (cap - 1);
+  }
+  return -3;
+}
+
+__device__ __forceinline__ double phase_ref(const double* phase,
+                                            const double* refph, int sub,
+                                            int64_t s, int a, int A, int D,
+                                            int d) {
+  double v = phase[s * D + d];
+  if (refph) v -= refph[(s / A) * D + d];
+  else if (sub >= 0) v -= phase[(s + (sub - a)) * D + d];
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// 1. classify slots, initialise the per-slot state, insert initial masks
+//    (one thread per slot)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void kl_classify_kernel(
+    const float* __restrict__ weight, int64_t S, int F, int A, int D,
+    const int* __restrict__ st_order, const uint8_t* __restrict__ skip,
+    int ref_skip, unsigned long long* __restrict__ keys, int cap,
+    int* __restrict__ pos, uint8_t* __restrict__ cls,
+    int* __restrict__ slow_list, int* __restrict__ counters,
+    double* __restrict__ coef, double* __restrict__ resid,
+    float* __restrict__ w_out, int32_t* __restrict__ order_out) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  const int a = (int)(s % A);
+  const int f = (int)((s / A) % F);
+  const float* w = weight + s * D;
+  for (int d = 0; d < D; ++d) {
+    coef[s * D + d] = 0.0;
+    resid[s * D + d] = 0.0;
+    w_out[s * D + d] = w[d];
+  }
+  if (a == ref_skip || skip[f * A + a]) {  // stationscreen.py:818-825
+    cls[s] = 1;
+    order_out[s] = 0;
+    pos[s] = -2;
+    return;
+  }
+  order_out[s] = st_order[a];
+  unsigned long long mask = 0ull;
+  bool tiny = false;
+  for (int d = 0; d < D; ++d) {
+    const float x = w[d];
+    if (x > 0.0f) mask |= 1ull << d;
+    tiny |= (x > 0.0f) && ((double)x <= kTinyW);
+  }
+  if (tiny) {
+    cls[s] = 2;
+    pos[s] = -2;
+    slow_list[atomicAdd(counters + 2, 1)] = (int)s;
+    return;
+  }
+  cls[s] = 0;
+  const unsigned long long full = (D == 64) ? ~0ull : ((1ull << D) - 1ull);
+  if (mask == full) pos[s] = -1;
+  else if (mask == 0ull) pos[s] = -2;
+  else pos[s] = table_insert(keys, cap, mask);
+}
+
+// 2. number the newly inserted masks (one thread per table entry)
+__global__ __launch_bounds__(256) void kl_assign_kernel(
+    const unsigned long long* __restrict__ keys, int cap, int* __restrict__ ids,
+    unsigned long long* __restrict__ pool_mask, int pool_cap,
+    int* __restrict__ counters) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cap) return;
+  const unsigned long long k = keys[i];
+  if (k != kEmptyKey && ids[i] < 0) {
+    const int id = atomicAdd(counters, 1);
+    ids[i] = id;
+    if (id < pool_cap) pool_mask[id] = k;
+  }
+}
+
+// 3. subset bases of the masks numbered [counters[1], counters[0]):
+//    C_sub = C[idx][:, idx] -> Jacobi -> U_sub sorted by |lambda| desc.
+__global__ __launch_bounds__(64) void kl_subset_eig_kernel(
+    const double* __restrict__ g_c, int D,
+    const unsigned long long* __restrict__ pool_mask, int pool_cap,
+    const int* __restrict__ counters, double* __restrict__ pool) {
+  extern __shared__ double smem[];
+  const int ld = ldo(D);
+  double* a = smem;
+  double* v = a + D * ld;
+  double2* cs = reinterpret_cast<double2*>(v + D * ld);
+  int* perm = reinterpret_cast<int*>(cs + 64);
+  int* idx = perm + 64;
+  const int first = counters[1];
+  const int last = min(counters[0], pool_cap);
+  const int l = lane();
+  for (int id = first + blockIdx.x; id < last; id += gridDim.x) {
+    const unsigned long long m = pool_mask[id];
+    const bool in = (l < D) && ((m >> l) & 1ull);
+    const int n = __popcll(m);
+    if (in) {
+      const int p = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+      idx[p] = l;
+    }
+    lds_sync();
+    if (l < n) {
+      const int r = idx[l];
+      for (int q = 0; q < n; ++q) a[l * ld + q] = g_c[r * D + idx[q]];
+    }
+    lds_sync();
+    wave_jacobi(a, v, cs, n, ld, 40);
+    wave_eig_order(a, n, ld, perm);
+    double* e = pool + (size_t)id * (D * D + D);
+    if (l < n) {
+      for (int r = 0; r < n; ++r) e[l * D + r] = v[l * ld + perm[r]];
+      const int pr = perm[l];
+      e[D * D + l] = a[pr * ld + pr];
+    }
+    lds_sync();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// 4. one fit pass (iteration `it` of _process_station) over all fast slots;
+//    one wavefront per slot.
+// ---------------------------------------------------------------------------
+struct FastLds {
+  const double* U;    // [D][ld] full basis, columns sorted
+  const double* C;    // [D][ld]
+  const double* lam;  // [64]
+  double* Vs;         // per wave: subset basis [D][ld]
+  double* lams;       // per wave [64]
+  double* G;          // per wave [D][ld]
+  double* vec;        // per wave [6][64]
+};
+
+__host__ __device__ inline size_t fast_shared_bytes(int D) {
+  return (size_t)(2 * D * ldo(D) + 64) * sizeof(double);
+}
+__host__ __device__ inline size_t fast_wave_bytes(int D) {
+  return (size_t)(2 * D * ldo(D) + 64 + 6 * 64) * sizeof(double);
+}
+
+struct Basis {
+  int n;
+  bool full;
+  const double* U;
+  const double* lam;
+};
+
+// One _fit_screen (stationscreen.py:433-594) in the eigenbasis.  Lanes p < n
+// carry the unflagged directions (phi_p, w_p); returns, per DIRECTION lane d,
+// white_d and resid_d.
+__device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
+                         int K, int screen_type, bool uniform, double wu,
+                         double phi_p, double w_p, double phi_d, double w_d,
+                         double& white_d, double& resid_d) {
+#pragma clang fp contract(off)
+  const int l = lane();
+  const int n = B.n;
+  double* v0 = L.vec;
+  double* v1 = L.vec + 64;
+  double* v2 = L.vec + 128;
+  double rc = 0.0, rs = 0.0;
+  if (l < n) {
+    if (screen_type == SF_SCREEN_PHASE) {
+      double sn, cn;
+      sincos(phi_p, &sn, &cn);
+      rc = w_p * cn;
+      rs = w_p * sn;
+    } else {
+      rc = w_p * phi_p;
+    }
+    v0[l] = rc;
+    v1[l] = rs;
+    v2[l] = w_p;
+  }
+  lds_sync();
+  double a1 = 0.0, a2 = 0.0;
+  if (l < K) {
+    for (int p = 0; p < n; ++p) {
+      const double u = B.U[p * ld + l];
+      a1 += u * v0[p];
+      a2 += u * v1[p];
+    }
+  }
+  if (K > 0) {
+    if (uniform) {
+      // U_k^T (w I) U_k = w I  (U_k orthonormal over the unflagged rows)
+      a1 /= wu;
+      a2 /= wu;
+    } else {
+      if (l < K) {
+        for (int j = 0; j < K; ++j) {
+          double s = 0.0;
+          for (int p = 0; p < n; ++p)
+            s += B.U[p * ld + l] * (v2[p] * B.U[p * ld + j]);
+          L.G[l * ld + j] = s;
+        }
+      }
+      lds_sync();
+      wave_cholesky_solve2(L.G, K, ld, a1, a2);
+    }
+  }
+  lds_sync();
+  // C re = U_k m(a): keep the components whose eigenvalue survives the cutoff
+  if (l < K) {
+    const bool keep = fabs(B.lam[l]) > kAtol;
+    v0[l] = keep ? a1 : 0.0;
+    v1[l] = keep ? a2 : 0.0;
+  }
+  lds_sync();
+  double screen = 0.0;
+  if (l < n) {
+    double cre = 0.0, cim = 0.0;
+    for (int k = 0; k < K; ++k) {
+      const double u = B.U[l * ld + k];
+      cre += u * v0[k];
+      cim += u * v1[k];
+    }
+    if (screen_type == SF_SCREEN_PHASE) {
+      screen = atan2(cim, cre);
+    } else {
+      screen = cre;
+    }
+  }
+  lds_sync();
+  if (l < n) v2[l] = screen;
+  lds_sync();
+  // s_hat = U^T screen; white = U Lambda^+ s_hat; C white = U (Lambda Lambda^+) s_hat
+  if (l < n) {
+    double sh = 0.0;
+    for (int p = 0; p < n; ++p) sh += B.U[p * ld + l] * v2[p];
+    const double lm = B.lam[l];
+    const bool keep = fabs(lm) > kAtol;
+    v0[l] = keep ? sh / lm : 0.0;
+    v1[l] = keep ? sh : 0.0;
+  }
+  lds_sync();
+  double white = 0.0, cw = 0.0;
+  if (l < n) {
+    for (int r = 0; r < n; ++r) {
+      const double u = B.U[l * ld + r];
+      white += u * v0[r];
+      cw += u * v1[r];
+    }
+  }
+  lds_sync();
+  if (B.full) {
+    white_d = white;
+    resid_d = phi_d - cw;
+    return;
+  }
+  // flagged directions (stationscreen.py:565-582): screen from the subset's
+  // white coefficients, then re-whitened with the full pinv(C)
+  if (l < n) {
+    v0[l] = screen;
+    v1[l] = white;
+  }
+  lds_sync();
+  const bool unfl = (l < D) && (w_d > 0.0);
+  const unsigned long long m = __ballot(unfl);
+  double sall = 0.0;
+  if (l < D) {
+    if (unfl) {
+      const int p = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+      sall = v0[p];
+    } else {
+      // C[l][idx p]: idx p = p-th set bit of m
+      unsigned long long mm = m;
+      int p = 0;
+      while (mm) {
+        const int q = __builtin_ctzll(mm);
+        sall += L.C[l * ld + q] * v1[p];
+        mm &= mm - 1;
+        ++p;
+      }
+    }
+  }
+  lds_sync();
+  if (l < D) v2[l] = sall;
+  lds_sync();
+  if (l < D) {
+    double sh = 0.0;
+    for (int p = 0; p < D; ++p) sh += L.U[p * ld + l] * v2[p];
+    const double lm = L.lam[l];
+    v0[l] = fabs(lm) > kAtol ? sh / lm : 0.0;
+  }
+  lds_sync();
+  double wa = 0.0;
+  if (l < D)
+    for (int r = 0; r < D; ++r) wa += L.U[l * ld + r] * v0[r];
+  lds_sync();
+  white_d = wa;
+  resid_d = phi_d - sall;
+}
+
+__global__ __launch_bounds__(256) void kl_fit_pass_kernel(
+    int it, int niter, int64_t S, int F, int A, int D,
+    const double* __restrict__ phase, const double* __restrict__ refph,
+    int ref_sub, const double* __restrict__ g_u, const double* __restrict__ g_c,
+    const double* __restrict__ g_eig, const int* __restrict__ st_order,
+    uint8_t* __restrict__ cls, int* __restrict__ pos,
+    const int* __restrict__ ids, unsigned long long* __restrict__ keys, int cap,
+    const double* __restrict__ pool, int pool_cap,
+    int* __restrict__ slow_list, int* __restrict__ counters, int screen_type,
+    double nsigma, int adjust_order, double* __restrict__ coef,
+    double* __restrict__ resid, float* __restrict__ w_out,
+    int32_t* __restrict__ order_out) {
+#pragma clang fp contract(off)
+  extern __shared__ double smem[];
+  const int ld = ldo(D);
+  const int nwaves = blockDim.x / 64;
+  const int wv = threadIdx.x / 64;
+  const int d = lane();
+  double* sU = smem;
+  double* sC = sU + D * ld;
+  double* sl = sC + D * ld;
+  for (int e = threadIdx.x; e < D * D; e += blockDim.x) {
+    const int r = e / D, c = e % D;
+    sU[r * ld + c] = g_u[e];
+    sC[r * ld + c] = g_c[e];
+  }
+  for (int e = threadIdx.x; e < 64; e += blockDim.x) sl[e] = e < D ? g_eig[e] : 0.0;
+  __syncthreads();
+  FastLds L;
+  L.U = sU;
+  L.C = sC;
+  L.lam = sl;
+  double* wb = sl + 64 + (size_t)wv * (fast_wave_bytes(D) / sizeof(double));
+  L.Vs = wb;
+  L.G = wb + D * ld;
+  L.lams = L.G + D * ld;
+  L.vec = L.lams + 64;
+
+  for (int64_t s = (int64_t)blockIdx.x * nwaves + wv; s < S;
+       s += (int64_t)gridDim.x * nwaves) {
+    if (cls[s] != 0) continue;
+    const int a = (int)(s % A);
+    int p0 = pos[s];
+    // basis of the current mask
+    int id = -1;
+    if (p0 >= 0) {
+      id = ids[p0];
+      if (id < 0 || id >= pool_cap) {  // pool overflow: general kernel
+        if (d == 0) {
+          cls[s] = 2;
+          slow_list[atomicAdd(counters + 2, 1)] = (int)s;
+        }
+        continue;
+      }
+    } else if (p0 == -3) {  // hash table full: general kernel
+      if (d == 0) {
+        cls[s] = 2;
+        slow_list[atomicAdd(counters + 2, 1)] = (int)s;
+      }
+      continue;
+    }
+    const int64_t base = s * D;
+    double phi_d = 0.0, w_d = 0.0;
+    if (d < D) {
+      phi_d = phase_ref(phase, refph, ref_sub, s, a, A, D, d);
+      w_d = (double)w_out[base + d];
+    }
+    double white_d = (d < D) ? coef[base + d] : 0.0;
+    double resid_d = (d < D) ? resid[base + d] : 0.0;
+    double order = (double)order_out[s];
+    const double station_order = (double)st_order[a];
+    const bool unfl = (d < D) && (w_d > 0.0);
+    const unsigned long long um = __ballot(unfl);
+    const int n_unfl = __popcll(um);
+
+    Basis B;
+    B.n = n_unfl;
+    B.full = (n_unfl == D);
+    if (B.full) {
+      B.U = L.U;
+      B.lam = L.lam;
+    } else if (n_unfl > 0) {
+      const double* e = pool + (size_t)id * (D * D + D);
+      for (int r = 0; r < n_unfl; ++r)
+        if (d < n_unfl) L.Vs[r * ld + d] = e[r * D + d];
+      if (d < n_unfl) L.lams[d] = e[D * D + d];
+      lds_sync();
+      B.U = L.Vs;
+      B.lam = L.lams;
+    }
+    // unflagged directions onto lanes p < n
+    double phi_p = 0.0, w_p = 0.0;
+    {
+      double* v4 = L.vec + 256;
+      double* v5 = L.vec + 320;
+      if (unfl) {
+        const int p = __builtin_amdgcn_mbcnt_hi((uint32_t)(um >> 32),
+                                                __builtin_amdgcn_mbcnt_lo((uint32_t)um, 0));
+        v4[p] = phi_d;
+        v5[p] = w_d;
+      }
+      lds_sync();
+      if (d < n_unfl) {
+        phi_p = v4[d];
+        w_p = v5[d];
+      }
+      lds_sync();
+    }
+    const double wmax = wave_max(unfl ? w_d : -INFINITY);
+    const double wmin = -wave_max(unfl ? -w_d : -INFINITY);
+    const bool uniform = (wmax == wmin);
+
+    if (n_unfl > 0) {
+      if (order > n_unfl - 1) order = n_unfl - 1;
+      if (it == 0) {
+        fit_once(L, B, D, ld, (int)order, screen_type, uniform, wmin, phi_p,
+                 w_p, phi_d, w_d, white_d, resid_d);
+      } else if (adjust_order) {
+        bool hit_upper = false, hit_lower = false, hit_upper2 = false,
+             hit_lower2 = false;
+        double sign = 1.0, prev_redchi2 = 0.0;
+        for (int oi = 0; oi < 4; ++oi) {
+          // oi == 0: the weights always compare equal (quirk Q2) -> no fit
+          if (oi > 0)
+            fit_once(L, B, D, ld, (int)order, screen_type, uniform, wmin,
+                     phi_p, w_p, phi_d, w_d, white_d, resid_d);
+          if (hit_lower2 || hit_upper2) break;
+          double redchi2;
+          if (screen_type == SF_SCREEN_PHASE) {
+            double sn = 0.0, cn = 0.0;
+            if (unfl) sincos(resid_d, &sn, &cn);
+            const double ww = unfl ? w_d : 0.0;
+            const double sw = wave_sum(ww);
+            const double m1 = wave_sum(sn * sn * ww) / sw;
+            const double m2 = wave_sum(cn * cn * ww) / sw;
+            redchi2 = (1.0 - hypot(m1, m2)) * sw / (n_unfl - order);
+          } else {
+            const double ww = unfl ? w_d : 0.0;
+            redchi2 = wave_sum(resid_d * resid_d * ww) / (n_unfl - order);
+          }
+          if (oi > 0) {
+            if (redchi2 > 1.0 && prev_redchi2 < redchi2) sign = -sign;
+            if (redchi2 < 1.0 && prev_redchi2 > redchi2) sign = -sign;
+          }
+          prev_redchi2 = redchi2;
+          const double order_factor = pow((double)n_unfl - order, 0.2);
+          double target = order - sign * order_factor * (1.0 - redchi2);
+          target = fmax(station_order, target);
+          target = fmin(rint(target), (double)(n_unfl - 1));
+          if (target <= 0.0) target = fmin(station_order, (double)(n_unfl - 1));
+          if (target == order) break;
+          if (target == n_unfl - 1) {
+            if (hit_upper) hit_upper2 = true;
+            hit_upper = true;
+          }
+          if (target == station_order) {
+            if (hit_lower) hit_lower2 = true;
+            hit_lower = true;
+          }
+          order = target;
+        }
+      }
+    }
+    // outlier flagging for the next pass (stationscreen.py:303-350, 660-671)
+    if (it + 1 < niter && screen_type == SF_SCREEN_PHASE) {
+      const bool live = d < D;
+      if (__any(live && w_d > 0.0)) {
+        double r = fmod(resid_d, 2.0 * M_PI);
+        if (r < -M_PI) r += 2.0 * M_PI;
+        if (r > M_PI) r -= 2.0 * M_PI;
+        const bool inc = live && (w_d != 0.0) && !isnan(r);
+        double sn = 0.0, cn = 0.0;
+        if (inc) sincos(r, &sn, &cn);
+        const double cnt = wave_sum(inc ? 1.0 : 0.0);
+        const double ms = wave_sum(sn) / cnt;
+        const double mc = wave_sum(cn) / cnt;
+        const double stdv = sqrt(-2.0 * log(hypot(ms, mc)));
+        const bool outl = live && (fabs(r) > nsigma * stdv);
+        if (outl) w_d = 0.0;
+        if (__any(outl)) {
+          const unsigned long long nm = __ballot(live && w_d > 0.0);
+          if (d == 0) pos[s] = (nm == 0ull) ? -2 : table_insert(keys, cap, nm);
+        }
+      }
+    }
+    if (d < D) {
+      coef[base + d] = white_d;
+      resid[base + d] = resid_d;
+      w_out[base + d] = (float)w_d;
+    }
+    if (d == 0) order_out[s] = (int32_t)order;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host orchestration
+// ---------------------------------------------------------------------------
+namespace {
+
+template <typename T>
+int grow(T** p, size_t& cap, size_t need, bool keep = false) {
+  if (*p && cap >= need) return SF_OK;
+  T* q = nullptr;
+  if (hipMalloc(reinterpret_cast<void**>(&q), need * sizeof(T)) != hipSuccess) {
+    set_error("hipMalloc failed (fit scratch)");
+    return SF_ENOMEM;
+  }
+  if (keep && *p && cap > 0)
+    hipMemcpy(q, *p, cap * sizeof(T), hipMemcpyDeviceToDevice);
+  if (*p) (void)hipFree(*p);
+  *p = q;
+  cap = need;
+  return SF_OK;
+}
+
+size_t next_pow2(size_t x) {
+  size_t p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+}  // namespace
+
+#define SF_TRYF(x)                 \
+  do {                             \
+    int rc_ = (x);                 \
+    if (rc_ != SF_OK) return rc_;  \
+  } while (0)
+
+static int ensure_pool(sf_ctx* ctx, size_t need) {
+  const size_t entry = (size_t)ctx->D * ctx->D + ctx->D;
+  if (ctx->pool_D != ctx->D) {
+    if (ctx->d_pool) (void)hipFree(ctx->d_pool);
+    if (ctx->d_pool_mask) (void)hipFree(ctx->d_pool_mask);
+    ctx->d_pool = nullptr;
+    ctx->d_pool_mask = nullptr;
+    ctx->pool_cap = 0;
+    ctx->pool_D = ctx->D;
+  }
+  if (ctx->pool_cap >= need) return SF_OK;
+  size_t cap = ctx->pool_cap ? ctx->pool_cap : 1024;
+  while (cap < need) cap *= 2;
+  size_t pc = ctx->pool_cap * entry, mc = ctx->pool_cap;
+  SF_TRYF(grow(&ctx->d_pool, pc, cap * entry, true));
+  SF_TRYF(grow(&ctx->d_pool_mask, mc, cap, true));
+  ctx->pool_cap = cap;
+  return SF_OK;
+}
+
+// pool_mask[id] for ids assigned beyond a previous pool capacity
+__global__ __launch_bounds__(256) void kl_fill_mask_kernel(
+    const unsigned long long* __restrict__ keys, const int* __restrict__ ids,
+    int cap, unsigned long long* __restrict__ pool_mask, int lo) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cap) return;
+  if (keys[i] != kEmptyKey && ids[i] >= lo) pool_mask[ids[i]] = keys[i];
+}
+
+// number new masks, make sure the pool holds them, decompose them
+static int number_and_decompose(sf_ctx* ctx) {
+  SF_HIP(hipMemcpyAsync(ctx->d_counters + 1, ctx->d_counters, sizeof(int),
+                        hipMemcpyDeviceToDevice, ctx->stream));
+  const int cap = (int)ctx->table_cap;
+  const int old_cap = (int)ctx->pool_cap;
+  hipLaunchKernelGGL(kl_assign_kernel, dim3((cap + 255) / 256), dim3(256), 0,
+                     ctx->stream, ctx->d_keys, cap, ctx->d_ids,
+                     ctx->d_pool_mask, old_cap, ctx->d_counters);
+  SF_HIP(hipGetLastError());
+  int cnt[2];
+  SF_HIP(hipMemcpyAsync(cnt, ctx->d_counters, 2 * sizeof(int),
+                        hipMemcpyDeviceToHost, ctx->stream));
+  SF_HIP(hipStreamSynchronize(ctx->stream));
+  if (cnt[0] > old_cap) {
+    SF_TRYF(ensure_pool(ctx, (size_t)cnt[0]));
+    hipLaunchKernelGGL(kl_fill_mask_kernel, dim3((cap + 255) / 256), dim3(256),
+                       0, ctx->stream, ctx->d_keys, ctx->d_ids, cap,
+                       ctx->d_pool_mask, old_cap);
+    SF_HIP(hipGetLastError());
+  }
+  const int n_new = cnt[0] - cnt[1];
+  if (n_new > 0) {
+    const int D = ctx->D;
+    const size_t shm = (size_t)2 * D * ldo(D) * sizeof(double) +
+                       64 * sizeof(double2) + 128 * sizeof(int);
+    if (shm > 64 * 1024)
+      SF_HIP(hipFuncSetAttribute(
+          reinterpret_cast<const void*>(&kl_subset_eig_kernel),
+          hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+    const int blocks = n_new < 8192 ? n_new : 8192;
+    hipLaunchKernelGGL(kl_subset_eig_kernel, dim3(blocks), dim3(64), shm,
+                       ctx->stream, ctx->d_c, D, ctx->d_pool_mask,
+                       (int)ctx->pool_cap, ctx->d_counters, ctx->d_pool);
+    SF_HIP(hipGetLastError());
+  }
+  return SF_OK;
+}
+
+int launch_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,
+               int F, int A, const sf_fit_params* p, double* coef,
+               double* resid, float* w_out, int32_t* order_out) {
+  const int D = ctx->D;
+  const int64_t S = (int64_t)T * F * A;
+  const RefSpec r = ref_spec(p, A);
+  SF_TRYF(launch_skip(ctx, phase, weight, T, F, A, r));
+
+  static const char* env = std::getenv("SCREENFIT_FIT");
+  if (ctx->force_general || (env && env[0] == 'g')) {
+    return launch_fit_general(ctx, nullptr, nullptr, S, phase, weight, T, F, A,
+                              p, r, coef, resid, w_out, order_out);
+  }
+  // scratch for outputs the caller does not want (they carry pass state)
+  if (!resid) {
+    SF_TRYF(grow(&ctx->d_scratch, ctx->scratch_cap, (size_t)S * D));
+    resid = ctx->d_scratch;
+  }
+  if (!w_out || !order_out) {
+    size_t wc = 0, oc = 0;
+    if (ctx->d_wscratch) (void)hipFree(ctx->d_wscratch);
+    if (ctx->d_oscratch) (void)hipFree(ctx->d_oscratch);
+    ctx->d_wscratch = nullptr;
+    ctx->d_oscratch = nullptr;
+    SF_TRYF(grow(&ctx->d_wscratch, wc, (size_t)S * D));
+    SF_TRYF(grow(&ctx->d_oscratch, oc, (size_t)S));
+    if (!w_out) w_out = ctx->d_wscratch;
+    if (!order_out) order_out = ctx->d_oscratch;
+  }
+  if (ctx->slot_cap < (size_t)S) {
+    size_t c1 = 0, c2 = 0, c3 = 0;
+    if (ctx->d_pos) (void)hipFree(ctx->d_pos);
+    if (ctx->d_slow) (void)hipFree(ctx->d_slow);
+    if (ctx->d_class) (void)hipFree(ctx->d_class);
+    ctx->d_pos = ctx->d_slow = nullptr;
+    ctx->d_class = nullptr;
+    SF_TRYF(grow(&ctx->d_pos, c1, (size_t)S));
+    SF_TRYF(grow(&ctx->d_slow, c2, (size_t)S));
+    SF_TRYF(grow(&ctx->d_class, c3, (size_t)S));
+    ctx->slot_cap = (size_t)S;
+  }
+  const size_t tcap = next_pow2((size_t)(2 * p->niter) * (size_t)S + 64);
+  if (ctx->table_cap < tcap) {
+    size_t c1 = 0, c2 = 0;
+    if (ctx->d_keys) (void)hipFree(ctx->d_keys);
+    if (ctx->d_ids) (void)hipFree(ctx->d_ids);
+    ctx->d_keys = nullptr;
+    ctx->d_ids = nullptr;
+    SF_TRYF(grow(&ctx->d_keys, c1, tcap));
+    SF_TRYF(grow(&ctx->d_ids, c2, tcap));
+    ctx->table_cap = tcap;
+  }
+  if (!ctx->d_counters) {
+    size_t c = 0;
+    SF_TRYF(grow(&ctx->d_counters, c, 4));
+  }
+  SF_TRYF(ensure_pool(ctx, 1024));
+  const int cap = (int)ctx->table_cap;
+  SF_HIP(hipMemsetAsync(ctx->d_keys, 0, ctx->table_cap * sizeof(unsigned long long),
+                        ctx->stream));
+  SF_HIP(hipMemsetAsync(ctx->d_ids, 0xff, ctx->table_cap * sizeof(int), ctx->stream));
+  SF_HIP(hipMemsetAsync(ctx->d_counters, 0, 4 * sizeof(int), ctx->stream));
+
+  hipLaunchKernelGGL(kl_classify_kernel, dim3((unsigned)((S + 255) / 256)),
+                     dim3(256), 0, ctx->stream, weight, S, F, A, D,
+                     ctx->d_st_order, ctx->d_skip, r.skip, ctx->d_keys, cap,
+                     ctx->d_pos, ctx->d_class, ctx->d_slow, ctx->d_counters,
+                     coef, resid, w_out, order_out);
+  SF_HIP(hipGetLastError());
+
+  const size_t shared = fast_shared_bytes(D);
+  const size_t wave = fast_wave_bytes(D);
+  int nw = 4;
+  while (nw > 1 && shared + nw * wave > 64 * 1024) --nw;
+  const size_t shm = shared + nw * wave;
+  if (shm > 64 * 1024)
+    SF_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&kl_fit_pass_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)shm));
+  int64_t blocks = (S + nw - 1) / nw;
+  if (blocks > 16384) blocks = 16384;
+  for (int it = 0; it < p->niter; ++it) {
+    SF_TRYF(number_and_decompose(ctx));
+    hipLaunchKernelGGL(kl_fit_pass_kernel, dim3((unsigned)blocks),
+                       dim3(64 * nw), shm, ctx->stream, it, p->niter, S, F, A,
+                       D, phase, r.refph, r.sub, ctx->d_u, ctx->d_c,
+                       ctx->d_eig, ctx->d_st_order, ctx->d_class, ctx->d_pos,
+                       ctx->d_ids, ctx->d_keys, cap, ctx->d_pool,
+                       (int)ctx->pool_cap, ctx->d_slow, ctx->d_counters,
+                       p->screen_type, p->nsigma, p->adjust_order, coef, resid,
+                       w_out, order_out);
+    SF_HIP(hipGetLastError());
+  }
+  // slow path: tiny weights / overflow, recomputed from scratch
+  return launch_fit_general(ctx, ctx->d_slow, ctx->d_counters + 2, S, phase,
+                            weight, T, F, A, p, r, coef, resid, w_out,
+                            order_out);
+}
+
+}  // namespace sf

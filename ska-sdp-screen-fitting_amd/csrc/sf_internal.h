@@ -61,9 +61,41 @@ struct sf_ctx {
   size_t skip_cap = 0;
   int* d_st_order = nullptr;   // [A]
   size_t st_order_cap = 0;
+  // mask-keyed cache of flagged-subset bases (kl_fit_fast.hip)
+  unsigned long long* d_keys = nullptr;  // hash table keys (0 = empty)
+  int* d_ids = nullptr;                  // hash table values (-1 = unassigned)
+  size_t table_cap = 0;                  // power of two
+  unsigned long long* d_pool_mask = nullptr;  // [pool_cap] mask of pool entry
+  double* d_pool = nullptr;              // [pool_cap][D*D + D] (U_sub, lam)
+  size_t pool_cap = 0;
+  int pool_D = 0;
+  int* d_pos = nullptr;                  // [S] table slot of the current mask
+  int* d_slow = nullptr;                 // [S] slow-path slot list
+  uint8_t* d_class = nullptr;            // [S] 0 fast, 1 skipped, 2 slow
+  size_t slot_cap = 0;
+  int* d_counters = nullptr;             // [0] ids, [1] range start, [2] slow
+  double* d_scratch = nullptr;           // resid / state when caller passes NULL
+  size_t scratch_cap = 0;
+  float* d_wscratch = nullptr;
+  int32_t* d_oscratch = nullptr;
+  // fast-path switch (SCREENFIT_FIT=general forces the general kernel)
+  int force_general = 0;
 };
 
 namespace sf {
+struct RefSpec {
+  int sub = -1;                 // local station whose phases are subtracted
+  const double* refph = nullptr;  // or: external reference phases [T][F][D]
+  int skip = -1;                // local station skipped as the reference
+};
+RefSpec ref_spec(const sf_fit_params* p, int A);
+int launch_skip(sf_ctx* ctx, const double* phase, const float* weight, int T,
+                int F, int A, const RefSpec& r);
+int launch_fit_general(sf_ctx* ctx, const int* slot_list, const int* n_list,
+                       int64_t max_slots, const double* phase,
+                       const float* weight, int T, int F, int A,
+                       const sf_fit_params* p, const RefSpec& r, double* coef,
+                       double* resid, float* w_out, int32_t* order_out);
 int launch_basis(sf_ctx* ctx);
 int launch_cpix(sf_ctx* ctx, const double* d_x, const double* d_y);
 int launch_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,

@@ -18,12 +18,14 @@ SF_SCREEN_TEC = 1
 SF_EVAL_NAN_SCRUB = 1
 SF_EVAL_FAST_SINCOS = 1 << 8
 SF_MAX_DIR = 60
+SF_OPT_FIT_GENERAL = 1
 
 # every symbol include/screenfit.h declares (checked by tests/test_capi.py)
 EXPORTED = (
     "sf_version", "sf_last_error", "sf_create", "sf_destroy", "sf_set_stream",
-    "sf_synchronize", "sf_alloc", "sf_free", "sf_copy_h2d", "sf_copy_d2h",
-    "sf_set_basis", "sf_get_basis", "sf_kl_fit", "sf_set_grid", "sf_kl_eval",
+    "sf_synchronize", "sf_set_option", "sf_alloc", "sf_free", "sf_copy_h2d", "sf_copy_d2h",
+    "sf_set_basis", "sf_get_basis", "sf_kl_fit", "sf_get_fit_stats",
+    "sf_set_grid", "sf_kl_eval",
 )
 
 
@@ -65,6 +67,7 @@ def load_library(path=None):
             "sf_destroy": ([vp], c_int),
             "sf_set_stream": ([vp, vp], c_int),
             "sf_synchronize": ([vp], c_int),
+            "sf_set_option": ([vp, c_int, c_int], c_int),
             "sf_alloc": ([vp, ctypes.c_size_t, ctypes.POINTER(vp)], c_int),
             "sf_free": ([vp, vp], c_int),
             "sf_copy_h2d": ([vp, vp, vp, ctypes.c_size_t], c_int),
@@ -73,6 +76,7 @@ def load_library(path=None):
             "sf_get_basis": ([vp, vp, vp, vp, vp], c_int),
             "sf_kl_fit": ([vp, vp, vp, c_int, c_int, c_int, ip,
                            ctypes.POINTER(FitParams), vp, vp, vp, vp], c_int),
+            "sf_get_fit_stats": ([vp, ip, ip], c_int),
             "sf_set_grid": ([vp, vp, c_int, vp, c_int], c_int),
             "sf_kl_eval": ([vp, vp, i64, vp, i64, ctypes.c_uint], c_int),
         }
@@ -132,6 +136,10 @@ class Context:
     def set_stream(self, stream_handle):
         _check(self.lib.sf_set_stream(self.h, stream_handle), "sf_set_stream")
 
+    def set_option(self, option, value):
+        _check(self.lib.sf_set_option(self.h, int(option), int(value)),
+               "sf_set_option")
+
     def synchronize(self):
         _check(self.lib.sf_synchronize(self.h), "sf_synchronize")
 
@@ -168,6 +176,12 @@ class Context:
             ctypes.byref(prm), _ptr(coef), _ptr(resid), _ptr(w_out),
             _ptr(order_out)), "sf_kl_fit")
 
+    def fit_stats(self):
+        nm, ng = ctypes.c_int(), ctypes.c_int()
+        _check(self.lib.sf_get_fit_stats(self.h, ctypes.byref(nm), ctypes.byref(ng)),
+               "sf_get_fit_stats")
+        return {"n_masks": nm.value, "n_general": ng.value}
+
     def set_grid(self, x, y):
         x = np.ascontiguousarray(x, dtype=np.float64)
         y = np.ascontiguousarray(y, dtype=np.float64)
@@ -175,7 +189,8 @@ class Context:
                                     y.ctypes.data, y.size), "sf_set_grid")
         self.grid = (x.size, y.size)
 
-    def eval(self, coef, S, out, ring_slots=None, flags=SF_EVAL_NAN_SCRUB):
+    def eval(self, coef, S, out, ring_slots=None,
+             flags=SF_EVAL_NAN_SCRUB | SF_EVAL_FAST_SINCOS):
         ring = int(S if ring_slots is None else ring_slots)
         _check(self.lib.sf_kl_eval(self.h, _ptr(coef), int(S), _ptr(out),
                                    max(ring, 1), int(flags)), "sf_kl_eval")

@@ -14,9 +14,12 @@ import numpy as np
 
 from . import geometry
 from . import stationscreen
-from ._lib import SF_EVAL_NAN_SCRUB, get_context
+from ._lib import SF_EVAL_FAST_SINCOS, SF_EVAL_NAN_SCRUB, get_context
 from .h5parm import H5parm, get_reference_station
 from .screen import Screen
+
+# NaN scrub (screen.py:368-378) + fp64 range reduction / fp32 sincos
+DEFAULT_FLAGS = SF_EVAL_NAN_SCRUB | SF_EVAL_FAST_SINCOS
 
 
 def read_patch_names(skymodel_filename):
@@ -48,7 +51,7 @@ class KLEvaluator:
             self.ctx.set_basis(self.pp, r_0, beta)
             self.ctx.set_grid(x_coord, y_coord)
 
-    def eval_device(self, coef_dev, out_dev=None, flags=SF_EVAL_NAN_SCRUB):
+    def eval_device(self, coef_dev, out_dev=None, flags=DEFAULT_FLAGS):
         """coef_dev: device [S, D] float64 -> device [S, 4, ny, nx] float32."""
         torch = self.torch
         S = coef_dev.shape[0]
@@ -60,7 +63,7 @@ class KLEvaluator:
             self.ctx.eval(coef_dev, S, out_dev, S, flags)
         return out_dev
 
-    def eval_host(self, coef, flags=SF_EVAL_NAN_SCRUB):
+    def eval_host(self, coef, flags=DEFAULT_FLAGS):
         """coef: host [..., D] -> host float32 [..., 4, ny, nx]."""
         coef = np.ascontiguousarray(coef, np.float64)
         lead = coef.shape[:-1]

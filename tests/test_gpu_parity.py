@@ -93,6 +93,25 @@ def test_fit_vs_reference_golden(ctx, dev, golden):
     assert rerr[keep].max() <= 1e-8
 
 
+@pytest.mark.parametrize("name", ["synth20", "synth50", "synth12tiny"])
+def test_fit_fast_equals_general_path(ctx, dev, name):
+    from ska_sdp_screen_fitting_amd._lib import SF_OPT_FIT_GENERAL
+    g = load_golden(name)
+    fast = gpu_fit(ctx, dev, g)
+    ctx.set_option(SF_OPT_FIT_GENERAL, 1)
+    try:
+        gen = gpu_fit(ctx, dev, g)
+    finally:
+        ctx.set_option(SF_OPT_FIT_GENERAL, 0)
+    np.testing.assert_array_equal(fast[3], gen[3])
+    np.testing.assert_array_equal(fast[2], gen[2])
+    bad = _ill_conditioned(g)
+    keep = np.ones(fast[0].shape[:3], bool)
+    for i in bad:
+        keep[i] = False
+    np.testing.assert_allclose(fast[0][keep], gen[0][keep], rtol=0, atol=1e-9)
+
+
 def test_fit_vs_oracle_config3_shape(ctx, dev):
     """A larger config-3-shaped synthetic (flags, outliers, adapted orders)."""
     from ska_sdp_screen_fitting_amd import geometry
@@ -147,7 +166,7 @@ def gpu_eval(ctx, dev, pp, x, y, coef_slots, flags=1, ring=None):
 def test_eval_vs_reference_golden(ctx, dev, golden, fast):
     from ska_sdp_screen_fitting_amd._lib import SF_EVAL_FAST_SINCOS
     g = golden
-    tol = 2e-6 if fast else 1e-6
+    tol = 1e-6
     flags = 1 | (SF_EVAL_FAST_SINCOS if fast else 0)
     for k, (f, s) in enumerate(g["pairs17"]):
         out = gpu_eval(ctx, dev, g["piercepoints"], g["x17"], g["y17"],
@@ -194,8 +213,11 @@ def test_eval_ring_and_nan_scrub(ctx, dev):
     out = gpu_eval(ctx, dev, g["piercepoints"], g["x17"], g["y17"], coef, ring=R)
     full = gpu_eval(ctx, dev, g["piercepoints"], g["x17"], g["y17"], coef)
     assert np.all(full[7, 0] == 1.0) and np.all(full[7, 1] == 0.0)
-    for s in range(50 - R, 50):
-        np.testing.assert_array_equal(out[s % R], full[s])
+    # each ring entry holds one of the slots that map to it (which one is
+    # unspecified: slots are written concurrently)
+    for r in range(R):
+        cands = [full[s] for s in range(r, 50, R)]
+        assert any(np.array_equal(out[r], c) for c in cands), r
     # without the scrub flag NaNs stay NaNs
     raw = gpu_eval(ctx, dev, g["piercepoints"], g["x17"], g["y17"], coef, flags=0)
     assert np.all(np.isnan(raw[7]))
