@@ -140,7 +140,8 @@ def main():
 
     from ska_sdp_screen_fitting_amd import get_context
     from ska_sdp_screen_fitting_amd._lib import (SF_EVAL_FAST_SINCOS,
-                                                 SF_EVAL_NAN_SCRUB)
+                                                 SF_EVAL_NAN_SCRUB,
+                                                 SF_EVAL_NT_STORES)
     from ska_sdp_screen_fitting_amd.distributed import setup_shard
     from ska_sdp_screen_fitting_amd.synthetic import (FIELD_DEC_DEG,
                                                       FIELD_RA_DEG,
@@ -172,7 +173,8 @@ def main():
     slot_bytes = 16 * P
     ring = int(min(S, max(1, args.ring_gb * 2 ** 30 // slot_bytes)))
     out = torch.empty((ring, 4, N, N), dtype=torch.float32, device=dev)
-    flags = SF_EVAL_NAN_SCRUB | (0 if args.precise_sincos else SF_EVAL_FAST_SINCOS)
+    flags = (SF_EVAL_NAN_SCRUB | SF_EVAL_NT_STORES
+             | (0 if args.precise_sincos else SF_EVAL_FAST_SINCOS))
 
     def fit():
         ctx.fit(phase, weight, T, F, A, setup["st_order"], niter=2,
@@ -228,7 +230,8 @@ def main():
         if os.path.exists(tpath):
             try:
                 tj = json.load(open(tpath))
-                if tj.get("workload") == args.workload:
+                if (tj.get("workload") == args.workload
+                        and tj.get("flags") == flags):
                     traffic = tj.get("hbm_bytes_per_launch")
             except (ValueError, OSError):
                 traffic = None

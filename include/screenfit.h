@@ -63,7 +63,8 @@ extern "C" {
 /* sf_kl_eval flags */
 #define SF_EVAL_NAN_SCRUB 1u /* NaN -> 1 (real planes), 0 (imag) (screen.py:368-378) */
 #define SF_EVAL_FAST_SINCOS (1u << 8) /* fp64 range reduction + fp32 sincos
-                                         (|err| <= 2e-7) instead of fp64 sincos */
+                                         (|err| <= 3e-7) instead of fp64 sincos */
+#define SF_EVAL_NT_STORES (1u << 9) /* non-temporal (streaming) cube stores */
 
 typedef struct sf_ctx sf_ctx;
 

@@ -69,9 +69,9 @@ __global__ __launch_bounds__(256) void kl_cpix_kernel(
   cfrag[e] = v;
 }
 
-__device__ __forceinline__ void jones_sincos(double ph, bool fast, float& s,
-                                             float& c) {
-  if (fast) {
+template <bool FAST>
+__device__ __forceinline__ void jones_sincos(double ph, float& s, float& c) {
+  if (FAST) {
     // exact-ish fp64 reduction to [-pi, pi], then fp32 sincos
     const double k = rint(ph * 0.15915494309189535);
     double r = fma(-k, 6.283185307179586, ph);
@@ -85,11 +85,19 @@ __device__ __forceinline__ void jones_sincos(double ph, bool fast, float& s,
   }
 }
 
-template <int KS, bool VEC4>
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ __forceinline__ void store4(float* p, v4f v) {
+  if (NT) __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(p));
+  else *reinterpret_cast<v4f*>(p) = v;
+}
+
+template <int KS, bool VEC4, bool FAST, bool NT>
 __global__ __launch_bounds__(256) void kl_eval_kernel(
     const double* __restrict__ cfrag, const double* __restrict__ coef, int D,
     int64_t S, int64_t P, int64_t n_pb, int64_t n_sc, int chunk_groups,
-    float* __restrict__ out, int64_t ring, unsigned flags, int fast) {
+    float* __restrict__ out, int64_t ring, unsigned flags) {
   const int l = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   // XCD-aware block -> (pixel block, slot chunk)
@@ -117,7 +125,6 @@ __global__ __launch_bounds__(256) void kl_eval_kernel(
       bf[kk][t] = cfrag[((wpb * KS + kk) * kTiles + t) * 64 + l];
 
   const bool scrub = flags & SF_EVAL_NAN_SCRUB;
-  const bool fst = fast != 0;
   const int64_t slot_base = sc * (int64_t)chunk_groups * 16;
   for (int g = 0; g < chunk_groups; ++g) {
     const int64_t s0 = slot_base + (int64_t)g * 16;
@@ -147,7 +154,7 @@ __global__ __launch_bounds__(256) void kl_eval_kernel(
       float cv[kTiles], sv[kTiles];
 #pragma unroll
       for (int t = 0; t < kTiles; ++t) {
-        jones_sincos(acc[t][r], fst, sv[t], cv[t]);
+        jones_sincos<FAST>(acc[t][r], sv[t], cv[t]);
         if (scrub) {
           if (isnan(cv[t])) cv[t] = 1.0f;
           if (isnan(sv[t])) sv[t] = 0.0f;
@@ -155,12 +162,12 @@ __global__ __launch_bounds__(256) void kl_eval_kernel(
       }
       float* o = out + ((s % ring) * 4) * P + p0;
       if (VEC4) {
-        const float4 c4 = make_float4(cv[0], cv[1], cv[2], cv[3]);
-        const float4 s4 = make_float4(sv[0], sv[1], sv[2], sv[3]);
-        *reinterpret_cast<float4*>(o) = c4;
-        *reinterpret_cast<float4*>(o + P) = s4;
-        *reinterpret_cast<float4*>(o + 2 * P) = c4;
-        *reinterpret_cast<float4*>(o + 3 * P) = s4;
+        const v4f c4 = {cv[0], cv[1], cv[2], cv[3]};
+        const v4f s4 = {sv[0], sv[1], sv[2], sv[3]};
+        store4<NT>(o, c4);
+        store4<NT>(o + P, s4);
+        store4<NT>(o + 2 * P, c4);
+        store4<NT>(o + 3 * P, s4);
       } else {
 #pragma unroll
         for (int t = 0; t < kTiles; ++t) {
@@ -201,15 +208,22 @@ static int launch_eval_ks(sf_ctx* ctx, const double* coef, int64_t S,
   int64_t nblk = n_pb * n_sc;
   if ((n_pb & 7) == 0) nblk = ((nblk + 7) / 8) * 8;
   const bool vec4 = (P % 4 == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
-  const int fast = (flags >> 8) & 1;
-  if (vec4)
-    hipLaunchKernelGGL((kl_eval_kernel<KS, true>), dim3((unsigned)nblk),
-                       dim3(256), 0, ctx->stream, ctx->d_cfrag, coef, ctx->D,
-                       S, P, n_pb, n_sc, groups, out, ring, flags, fast);
-  else
-    hipLaunchKernelGGL((kl_eval_kernel<KS, false>), dim3((unsigned)nblk),
-                       dim3(256), 0, ctx->stream, ctx->d_cfrag, coef, ctx->D,
-                       S, P, n_pb, n_sc, groups, out, ring, flags, fast);
+  const bool fast = flags & SF_EVAL_FAST_SINCOS;
+  const bool nt = flags & SF_EVAL_NT_STORES;
+#define SF_LAUNCH(V, F, N)                                                     \
+  hipLaunchKernelGGL((kl_eval_kernel<KS, V, F, N>), dim3((unsigned)nblk),      \
+                     dim3(256), 0, ctx->stream, ctx->d_cfrag, coef, ctx->D, S, \
+                     P, n_pb, n_sc, groups, out, ring, flags)
+  if (vec4) {
+    if (fast) {
+      if (nt) SF_LAUNCH(true, true, true); else SF_LAUNCH(true, true, false);
+    } else {
+      if (nt) SF_LAUNCH(true, false, true); else SF_LAUNCH(true, false, false);
+    }
+  } else {
+    if (fast) SF_LAUNCH(false, true, false); else SF_LAUNCH(false, false, false);
+  }
+#undef SF_LAUNCH
   SF_HIP(hipGetLastError());
   return SF_OK;
 }

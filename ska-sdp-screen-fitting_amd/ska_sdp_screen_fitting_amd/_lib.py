@@ -17,6 +17,7 @@ SF_SCREEN_PHASE = 0
 SF_SCREEN_TEC = 1
 SF_EVAL_NAN_SCRUB = 1
 SF_EVAL_FAST_SINCOS = 1 << 8
+SF_EVAL_NT_STORES = 1 << 9
 SF_MAX_DIR = 60
 SF_OPT_FIT_GENERAL = 1
 
@@ -190,7 +191,7 @@ class Context:
         self.grid = (x.size, y.size)
 
     def eval(self, coef, S, out, ring_slots=None,
-             flags=SF_EVAL_NAN_SCRUB | SF_EVAL_FAST_SINCOS):
+             flags=SF_EVAL_NAN_SCRUB | SF_EVAL_FAST_SINCOS | SF_EVAL_NT_STORES):
         ring = int(S if ring_slots is None else ring_slots)
         _check(self.lib.sf_kl_eval(self.h, _ptr(coef), int(S), _ptr(out),
                                    max(ring, 1), int(flags)), "sf_kl_eval")

@@ -14,12 +14,14 @@ import numpy as np
 
 from . import geometry
 from . import stationscreen
-from ._lib import SF_EVAL_FAST_SINCOS, SF_EVAL_NAN_SCRUB, get_context
+from ._lib import (SF_EVAL_FAST_SINCOS, SF_EVAL_NAN_SCRUB, SF_EVAL_NT_STORES,
+                   get_context)
 from .h5parm import H5parm, get_reference_station
 from .screen import Screen
 
-# NaN scrub (screen.py:368-378) + fp64 range reduction / fp32 sincos
-DEFAULT_FLAGS = SF_EVAL_NAN_SCRUB | SF_EVAL_FAST_SINCOS
+# NaN scrub (screen.py:368-378) + fp64 range reduction / fp32 sincos +
+# streaming stores
+DEFAULT_FLAGS = SF_EVAL_NAN_SCRUB | SF_EVAL_FAST_SINCOS | SF_EVAL_NT_STORES
 
 
 def read_patch_names(skymodel_filename):

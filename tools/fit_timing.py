@@ -9,7 +9,7 @@ import torch
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "ska-sdp-screen-fitting_amd"))
 from ska_sdp_screen_fitting_amd import geometry, get_context  # noqa: E402
-from ska_sdp_screen_fitting_amd._lib import SF_EVAL_FAST_SINCOS  # noqa: E402
+from ska_sdp_screen_fitting_amd._lib import SF_EVAL_FAST_SINCOS, SF_EVAL_NT_STORES  # noqa: E402
 from ska_sdp_screen_fitting_amd.stationscreen import station_orders  # noqa: E402
 from ska_sdp_screen_fitting_amd.synthetic import make_solutions  # noqa: E402
 
@@ -57,7 +57,8 @@ def main():
     ring = 16384
     out = torch.empty((ring, 4, 256, 256), dtype=torch.float32, device=dev)
     for flags, name in ((1, "fp64 sincos+scrub"), (0, "fp64 sincos"),
-                        (1 | SF_EVAL_FAST_SINCOS, "fast sincos+scrub")):
+                        (1 | SF_EVAL_FAST_SINCOS, "fast sincos+scrub"),
+                        (1 | SF_EVAL_FAST_SINCOS | SF_EVAL_NT_STORES, "fast+scrub+nt")):
         ms = timeit(lambda: ctx.eval(coef, S, out, ring, flags))
         gbs = S * (16 * 65536 + 160) / (ms * 1e-3) / 1e9
         print(f"eval {name:18s}: {ms:8.2f} ms  {gbs:8.1f} GB/s", flush=True)
