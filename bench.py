@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--cpu-workers", type=int, default=16)
     ap.add_argument("--eval-only", action="store_true",
                     help="time only sf_kl_eval (profiling)")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="gloo: rehearse N ranks on a 1-GPU box (setup "
+                         "collectives on the CPU, ranks share the device)")
     return ap.parse_args()
 
 
@@ -133,10 +136,16 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    n_dev = torch.cuda.device_count()
+    gpu = local_rank if args.dist_backend == "nccl" else local_rank % max(n_dev, 1)
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     from ska_sdp_screen_fitting_amd import get_context
     from ska_sdp_screen_fitting_amd._lib import (SF_EVAL_FAST_SINCOS,
@@ -152,10 +161,11 @@ def main():
     sol = make_solutions(n_ant=A, n_time=T, n_freq=F, n_dir=D,
                          ant_offset=A * rank, n_ant_total=A * world)
     setup = setup_shard(sol, A * rank, A * world, FIELD_RA_DEG, FIELD_DEC_DEG,
-                        FIELD_WIDTH_DEG, cell, device=dev if world > 1 else "cpu")
+                        FIELD_WIDTH_DEG, cell,
+                        device=coll_dev if world > 1 else "cpu")
     assert len(setup["x"]) == N
 
-    ctx = get_context(local_rank)
+    ctx = get_context(gpu)
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)
     ctx.set_basis(setup["piercepoints"], 100, 5.0 / 3.0)
@@ -213,12 +223,12 @@ def main():
     fit_stats = ctx.fit_stats() if not args.eval_only else {}
     t_fit = float(np.mean([a.elapsed_time(b) for a, b, _ in ev])) * 1e-3
     t_eval = float(np.mean([b.elapsed_time(c) for _, b, c in ev])) * 1e-3
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
     if world > 1:
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     elapsed = tmax.item()
 
-    # parity spot check (cheap invariants, not timed): |cos|^2 + |sin|^2 = 1
+    # parity spot check (cheap invariants, not timed): cos^2 + sin^2 = 1
     chk = out[: min(ring, 64)].float()
     unit_err = float((chk[:, 0] ** 2 + chk[:, 1] ** 2 - 1).abs().max())
 

@@ -30,6 +30,10 @@ namespace sf {
 
 typedef double v4d __attribute__((ext_vector_type(4)));
 
+#ifndef SF_EVAL_MIN_WAVES
+#define SF_EVAL_MIN_WAVES 2
+#endif
+
 
 // f64 16x16x4 accumulator layout on gfx950: lane l, register r holds
 // D[row = (l >> 4) + 4 r][col = l & 15] (cdna_hip_programming.md §3).
@@ -94,7 +98,7 @@ __device__ __forceinline__ void store4(float* p, v4f v) {
 }
 
 template <int KS, bool VEC4, bool FAST, bool NT>
-__global__ __launch_bounds__(256) void kl_eval_kernel(
+__global__ __launch_bounds__(256, SF_EVAL_MIN_WAVES) void kl_eval_kernel(
     const double* __restrict__ cfrag, const double* __restrict__ coef, int D,
     int64_t S, int64_t P, int64_t n_pb, int64_t n_sc, int chunk_groups,
     float* __restrict__ out, int64_t ring, unsigned flags) {

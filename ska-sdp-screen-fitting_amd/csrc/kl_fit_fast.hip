@@ -354,7 +354,10 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
   resid_d = phi_d - sall;
 }
 
-__global__ __launch_bounds__(256) void kl_fit_pass_kernel(
+#ifndef SF_FIT_MIN_WAVES
+#define SF_FIT_MIN_WAVES 1
+#endif
+__global__ __launch_bounds__(256, SF_FIT_MIN_WAVES) void kl_fit_pass_kernel(
     int it, int niter, int64_t S, int F, int A, int D,
     const double* __restrict__ phase, const double* __restrict__ refph,
     int ref_sub, const double* __restrict__ g_u, const double* __restrict__ g_c,

@@ -43,9 +43,10 @@ __device__ __forceinline__ int rr_partner(int i, int r, int m) {
   const int mm = m - 1;
   if (i == mm) return r;
   if (i == r) return mm;
+  // 2r - i lies in (-mm, 2mm): one conditional add / subtract, no modulo
   int p = 2 * r - i;
-  p %= mm;
   if (p < 0) p += mm;
+  if (p >= mm) p -= mm;
   return p;
 }
 
