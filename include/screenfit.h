@@ -153,6 +153,20 @@ int sf_set_grid(sf_ctx* ctx, const double* x_host, int nx,
 int sf_kl_eval(sf_ctx* ctx, const double* coef, int64_t S, float* out,
                int64_t ring_slots, unsigned flags);
 
+/*
+ * Tessellated (Voronoi) screens: fill every pixel with the values of the
+ * direction whose cell contains it, then (smooth_pix > 0) apply the Gaussian
+ * of Screen.write.  Replaces VoronoiScreen.make_matrix + the smoothing loop
+ * (voronoi_screen.py:132-216, screen.py:353-362).  Device inputs: labels
+ * [ny][nx] int32 in 1..D (the template of make_rasertize_template), phase
+ * [S][D] float64 (already referenced), amp_xx / amp_yy [S][D] float64 or NULL
+ * (phase-only: amplitude 1).  Output as sf_kl_eval.  smooth_pix <= 6.
+ */
+int sf_tess_fill(sf_ctx* ctx, const int32_t* labels, int nx, int ny,
+                 const double* phase, const double* amp_xx,
+                 const double* amp_yy, int D, int64_t S, float* out,
+                 int64_t ring_slots, double smooth_pix, unsigned flags);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,6 +1,7 @@
 // capi.hip -- the extern "C" boundary of libscreenfit (include/screenfit.h).
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -98,6 +99,7 @@ int sf_destroy(sf_ctx* ctx) {
   hipFree(ctx->d_scratch);
   hipFree(ctx->d_wscratch);
   hipFree(ctx->d_oscratch);
+  hipFree(ctx->d_gw);
   delete ctx;
   return SF_OK;
 }
@@ -299,6 +301,43 @@ int sf_kl_eval(sf_ctx* ctx, const double* coef, int64_t S, float* out,
   if (S == 0) return SF_OK;
   SF_HIP(hipSetDevice(ctx->device));
   return sf::launch_eval(ctx, coef, S, out, ring, flags);
+}
+
+int sf_tess_fill(sf_ctx* ctx, const int32_t* labels, int nx, int ny,
+                 const double* phase, const double* amp_xx,
+                 const double* amp_yy, int D, int64_t S, float* out,
+                 int64_t ring, double smooth_pix, unsigned flags) {
+  SF_REQUIRE(ctx && labels && phase && out, SF_EINVAL, "sf_tess_fill: NULL argument");
+  SF_REQUIRE(nx >= 1 && ny >= 1 && D >= 1 && D <= 64 && S >= 0 && ring >= 1,
+             SF_EINVAL, "sf_tess_fill: bad shape");
+  SF_REQUIRE(smooth_pix >= 0.0 && smooth_pix <= 6.0, SF_EINVAL,
+             "sf_tess_fill: smooth_pix must be in [0, 6]");
+  if (S == 0) return SF_OK;
+  SF_HIP(hipSetDevice(ctx->device));
+  // scipy.ndimage._gaussian_kernel1d(sigma, 0, int(4 sigma + 0.5))
+  int R = 0;
+  std::vector<double> w(1, 1.0);
+  if (smooth_pix > 1e-15) {
+    R = (int)(4.0 * smooth_pix + 0.5);
+    w.assign(2 * R + 1, 0.0);
+    double sum = 0.0;
+    for (int i = -R; i <= R; ++i) {
+      w[i + R] = std::exp(-0.5 / (smooth_pix * smooth_pix) * (double)(i * i));
+    }
+    for (int i = 0; i < 2 * R + 1; ++i) sum += w[i];
+    for (int i = 0; i < 2 * R + 1; ++i) w[i] /= sum;
+  }
+  if (!ctx->d_gw) {
+    if (hipMalloc(reinterpret_cast<void**>(&ctx->d_gw), 64 * sizeof(double)) !=
+        hipSuccess) {
+      set_error("hipMalloc failed");
+      return SF_ENOMEM;
+    }
+  }
+  SF_HIP(hipMemcpyAsync(ctx->d_gw, w.data(), w.size() * sizeof(double),
+                        hipMemcpyHostToDevice, ctx->stream));
+  return sf::launch_tess(ctx, labels, nx, ny, phase, amp_xx, amp_yy, D, S,
+                         out, ring, ctx->d_gw, R, flags);
 }
 
 }  // extern "C"

@@ -78,6 +78,8 @@ struct sf_ctx {
   size_t scratch_cap = 0;
   float* d_wscratch = nullptr;
   int32_t* d_oscratch = nullptr;
+  // Gaussian weights of sf_tess_fill
+  double* d_gw = nullptr;
   // fast-path switch (SCREENFIT_FIT=general forces the general kernel)
   int force_general = 0;
 };
@@ -103,4 +105,8 @@ int launch_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,
                double* resid, float* w_out, int32_t* order_out);
 int launch_eval(sf_ctx* ctx, const double* coef, int64_t S, float* out,
                 int64_t ring, unsigned flags);
+int launch_tess(sf_ctx* ctx, const int32_t* labels, int nx, int ny,
+                const double* phase, const double* amp_xx,
+                const double* amp_yy, int D, int64_t S, float* out,
+                int64_t ring, const double* d_w, int R, unsigned flags);
 }  // namespace sf

@@ -26,7 +26,7 @@ EXPORTED = (
     "sf_version", "sf_last_error", "sf_create", "sf_destroy", "sf_set_stream",
     "sf_synchronize", "sf_set_option", "sf_alloc", "sf_free", "sf_copy_h2d", "sf_copy_d2h",
     "sf_set_basis", "sf_get_basis", "sf_kl_fit", "sf_get_fit_stats",
-    "sf_set_grid", "sf_kl_eval",
+    "sf_set_grid", "sf_kl_eval", "sf_tess_fill",
 )
 
 
@@ -80,6 +80,8 @@ def load_library(path=None):
             "sf_get_fit_stats": ([vp, ip, ip], c_int),
             "sf_set_grid": ([vp, vp, c_int, vp, c_int], c_int),
             "sf_kl_eval": ([vp, vp, i64, vp, i64, ctypes.c_uint], c_int),
+            "sf_tess_fill": ([vp, vp, c_int, c_int, vp, vp, vp, c_int, i64, vp,
+                              i64, c_dbl, ctypes.c_uint], c_int),
         }
         for name, (args, res) in sig.items():
             fn = getattr(lib, name)
@@ -195,6 +197,17 @@ class Context:
         ring = int(S if ring_slots is None else ring_slots)
         _check(self.lib.sf_kl_eval(self.h, _ptr(coef), int(S), _ptr(out),
                                    max(ring, 1), int(flags)), "sf_kl_eval")
+
+
+    def tess_fill(self, labels, nx, ny, phase, D, S, out, ring_slots=None,
+                  amp_xx=None, amp_yy=None, smooth_pix=0.0,
+                  flags=SF_EVAL_NAN_SCRUB):
+        ring = int(S if ring_slots is None else ring_slots)
+        _check(self.lib.sf_tess_fill(self.h, _ptr(labels), int(nx), int(ny),
+                                     _ptr(phase), _ptr(amp_xx), _ptr(amp_yy),
+                                     int(D), int(S), _ptr(out), max(ring, 1),
+                                     float(smooth_pix), int(flags)),
+               "sf_tess_fill")
 
 
 _contexts = {}

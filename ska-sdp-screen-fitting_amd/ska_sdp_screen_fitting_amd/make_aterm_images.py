@@ -1,10 +1,12 @@
 """``make_aterm_image`` -- the drop-in entry point (make_aterm_images.py:15-153
-of the reference), same signature and side effects, GPU-backed KL path."""
+of the reference), same signature and side effects, GPU-backed KL and
+tessellated paths."""
 
 import os
 
 from .h5parm import H5parm
 from .kl_screen import KLScreen
+from .voronoi_screen import VoronoiScreen
 
 
 def make_aterm_image(h5parmfile, soltabname="phase000", screen_type="tessellated",
@@ -53,9 +55,10 @@ def make_aterm_image(h5parmfile, soltabname="phase000", screen_type="tessellated
                           solset_name=solsetname, phase_soltab_name=soltab_ph,
                           amplitude_soltab_name=soltab_amp)
     elif screen_type == "tessellated":
-        raise NotImplementedError(
-            "tessellated (Voronoi) screens are the next row of the build "
-            "(SURVEY.md §8(f) rank 1)")
+        screen = VoronoiScreen(rootname, h5parmfile, skymodel, bounds_mid_deg[0],
+                               bounds_mid_deg[1], width_deg, width_deg,
+                               solset_name=solsetname, phase_soltab_name=soltab_ph,
+                               amplitude_soltab_name=soltab_amp)
     else:
         raise ValueError(f"unknown screen_type {screen_type!r}")
     screen.process(ncpu=ncpu)

@@ -1,0 +1,242 @@
+"""Tessellated (Voronoi) screens (voronoi_screen.py:24-351 of the reference).
+
+The label raster ("template") is host setup, computed once per run: patch
+positions from the sky model, SIN pixel coordinates, a Voronoi tessellation
+closed by a 64-point outer ring, one polygon per direction rasterized with
+Pillow exactly as ``utils/processing_utils.rasterize`` does (fill + outline
+with rounded vertices, then an exact border test of the outline pixels,
+quirk Q10) and a nearest-label fallback for uncovered pixels.  The per-slot
+work -- gather of each direction's (amplitude x) cos / sin into its cells and
+the optional Gaussian smoothing of ``Screen.write`` (screen.py:353-362) --
+runs in the HIP kernel ``kl_tess_kernel`` through ``sf_tess_fill``.
+"""
+
+import os
+
+import numpy as np
+import scipy.interpolate as si
+from PIL import Image, ImageDraw
+from scipy.spatial import Voronoi
+
+from . import fits, geometry
+from ._lib import SF_EVAL_NAN_SCRUB, get_context
+from .h5parm import H5parm, get_reference_station
+from .screen import Screen
+
+
+def parse_angle(text, hours):
+    """lsmtool patch-position strings: RA "hh:mm:ss.s", Dec "dd.mm.ss.s"."""
+    t = text.strip()
+    sign = -1.0 if t.startswith("-") else 1.0
+    t = t.lstrip("+-")
+    f = t.split(":") if ":" in t else t.split(".", 2)
+    val = float(f[0]) + float(f[1]) / 60.0 + float(f[2]) / 3600.0
+    return sign * val * (15.0 if hours else 1.0)
+
+
+def read_patch_positions(skymodel_filename):
+    """{patch name: (ra_deg, dec_deg)} from the patch lines of a sky model."""
+    out = {}
+    with open(skymodel_filename, encoding="utf8") as fh:
+        for line in fh:
+            p = [x.strip() for x in line.split(",")]
+            if len(p) == 5 and p[0] == "" and p[1] == "" and p[2]:
+                out[p[2]] = (parse_angle(p[3], True), parse_angle(p[4], False))
+    return out
+
+
+def _on_or_inside(ring, x, y):
+    """Not shapely-disjoint: winding number != 0 or on an edge."""
+    wn = 0
+    for (x0, y0), (x1, y1) in zip(ring[:-1], ring[1:]):
+        cr = (x1 - x0) * (y - y0) - (x - x0) * (y1 - y0)
+        if cr == 0.0 and min(x0, x1) <= x <= max(x0, x1) and \
+                min(y0, y1) <= y <= max(y0, y1):
+            return True
+        if y0 <= y < y1 and cr > 0:
+            wn += 1
+        elif y1 <= y < y0 and cr < 0:
+            wn -= 1
+    return wn != 0
+
+
+def rasterize_cell(ring, n):
+    """utils/processing_utils.py:295-334 for one closed ring, n x n image:
+    returns a boolean mask [y, x]."""
+    img = Image.new("L", (n, n), 0)
+    ImageDraw.Draw(img).polygon(ring, outline=1, fill=1)
+    mask = np.array(img) > 0
+    edge = Image.new("L", (n, n), 0)
+    ImageDraw.Draw(edge).polygon(ring, outline=1, fill=0)
+    ey, ex = np.nonzero(np.array(edge))
+    for x, y in zip(ex, ey):
+        if not _on_or_inside(ring, float(x), float(y)):
+            mask[y, x] = False
+    return mask
+
+
+def tessellation_template(patch_radec, rad, dec, width_deg, cellsize_deg):
+    """voronoi_screen.py:218-351 -> (labels [ny, nx] int32 in 1..D, patch xy).
+    Cells are painted in direction order (later cells win a shared pixel)."""
+    n = geometry.grid_size(width_deg, cellsize_deg)
+    crval, crpix, cdelt = (rad, dec), (n / 2.0, n / 2.0), (-cellsize_deg, cellsize_deg)
+    ra = np.asarray(patch_radec, np.float64)[:, 0]
+    de = np.asarray(patch_radec, np.float64)[:, 1]
+    xy = np.stack(geometry.sin_world2pix(ra, de, crval, crpix, cdelt), axis=1)
+    bnd = (rad + width_deg / 2.0, dec - width_deg / 2.0,
+           rad - width_deg / 2.0, dec + width_deg / 2.0)
+    x0, y0 = geometry.sin_world2pix(max(bnd[0], ra.max() + 0.1),
+                                    min(bnd[1], de.min() - 0.1), crval, crpix, cdelt)
+    x1, y1 = geometry.sin_world2pix(min(bnd[2], ra.min() - 0.1),
+                                    max(bnd[3], de.max() + 0.1), crval, crpix, cdelt)
+    x0, y0, x1, y1 = float(x0), float(y0), float(x1), float(y1)
+    if len(xy) == 1:
+        rings = [[(x0, y0), (x0, y1), (x1, y1), (x1, y0), (x0, y0)]]
+    else:
+        k = np.arange(64)
+        radius = 2.0 * np.hypot(x1 - x0, y1 - y0)
+        ring_pts = xy.mean(axis=0) + radius * np.stack(
+            [np.cos(np.pi / 32.0 * k), np.sin(np.pi / 32.0 * k)], axis=1)
+        vor = Voronoi(np.vstack([xy, ring_pts]))
+        rings = []
+        for i in range(len(xy)):
+            reg = vor.regions[vor.point_region[i]]
+            if -1 in reg:
+                raise ValueError("unbounded Voronoi cell for a direction")
+            v = vor.vertices[reg]
+            ctr = v.mean(axis=0)
+            v = v[np.argsort(np.arctan2(v[:, 1] - ctr[1], v[:, 0] - ctr[0]))]
+            pts = [(float(a), float(b)) for a, b in v]
+            rings.append(pts + [pts[0]])
+    labels = np.zeros((n, n), np.int32)
+    for i, ring in enumerate(rings):
+        labels[rasterize_cell(ring, n)] = i + 1
+    empty = labels == 0
+    if empty.any():
+        iy, ix = np.nonzero(~empty)
+        zy, zx = np.nonzero(empty)
+        labels[empty] = si.griddata((iy, ix), labels[~empty], (zy, zx),
+                                    method="nearest")
+    return labels, xy
+
+
+def gaussian_weights(smooth_pix, truncate=4.0):
+    """scipy.ndimage._gaussian_kernel1d (order 0): radius and weights."""
+    sigma = float(smooth_pix)
+    radius = int(truncate * sigma + 0.5)
+    x = np.arange(-radius, radius + 1)
+    phi = np.exp(-0.5 / (sigma * sigma) * x ** 2)
+    return radius, phi / phi.sum()
+
+
+class VoronoiScreen(Screen):
+    """Class for Voronoi screens (voronoi_screen.py:24)."""
+
+    def __init__(self, name, h5parm_filename, skymodel_filename, rad, dec,
+                 width_ra, width_dec, solset_name="sol000",
+                 phase_soltab_name="phase000", amplitude_soltab_name=None):
+        super().__init__(name, h5parm_filename, skymodel_filename, rad, dec,
+                         width_ra, width_dec, solset_name=solset_name,
+                         phase_soltab_name=phase_soltab_name,
+                         amplitude_soltab_name=amplitude_soltab_name)
+        self.data_rasertize_template = None
+        self.polygons = None
+        self._dev_cache = None
+
+    def fit(self):
+        """Reference the phases to one station (voronoi_screen.py:57-102)."""
+        if not self.phase_only:
+            raise NotImplementedError("gain (amplitude) tessellated screens: next row")
+        h5 = H5parm(self.input_h5parm_filename)
+        solset = h5.get_solset(self.input_solset_name)
+        st = solset.get_soltab(self.input_phase_soltab_name)
+        ref = get_reference_station(st, 10)
+        vals = np.array(st.val, dtype=np.float64)
+        vals = vals - vals[:, :, ref:ref + 1, :]
+        self.vals_ph = vals
+        self.times_ph = np.asarray(st.time)
+        self.freqs_ph = np.asarray(st.freq)
+        self.vals_amp = None  # ones (phase only)
+        self.times_amp, self.freqs_amp = self.times_ph, self.freqs_ph
+        self.source_names = st.dir
+        self.source_dict = solset.get_source()
+        self.source_positions = [self.source_dict[s] for s in self.source_names]
+        self.station_names = st.ant
+        self.station_dict = solset.get_ant()
+        self.station_positions = [self.station_dict[s] for s in self.station_names]
+        h5.close()
+
+    def get_memory_usage(self, cellsize_deg):
+        """voronoi_screen.py:104-130 (x10 overhead, no ncpu factor)."""
+        ximsize = int(self.width_ra / cellsize_deg)
+        yimsize = int(self.width_dec / cellsize_deg)
+        nbytes = 8 * len(self.freqs_ph) * len(self.station_names) * 4 * yimsize * ximsize
+        return nbytes / 1024 ** 3 * 10
+
+    def make_rasertize_template(self, cellsize_deg, out_dir):
+        """voronoi_screen.py:218-351; also writes {name}_template.fits."""
+        n = geometry.grid_size(self.width_ra, cellsize_deg)
+        path = os.path.join(out_dir, f"{self.name}_template.fits")
+        cards = fits.aterm_header(self.rad, self.dec, n, n, cellsize_deg,
+                                  self.freqs_ph, self.times_ph[0:1],
+                                  len(self.station_names))
+        w = fits.CubeWriter(path, cards, (1, len(self.freqs_ph),
+                                          len(self.station_names), 4, n, n))
+        w.write(np.zeros((1, len(self.freqs_ph), len(self.station_names), 4, n, n),
+                         np.float32))
+        w.close()
+        pos = read_patch_positions(self.input_skymodel_filename)
+        radec = np.array([pos[str(s).strip("[]")] for s in self.source_names])
+        self.data_rasertize_template, self.polygons = tessellation_template(
+            radec, self.rad, self.dec, self.width_ra, cellsize_deg)
+        self._dev_cache = None
+
+    def _device(self):
+        import torch
+        if self._dev_cache is None:
+            dev = torch.device("cuda", self.device)
+            lab = torch.from_numpy(self.data_rasertize_template.astype(np.int32)).to(dev)
+            self._dev_cache = (dev, lab)
+        return self._dev_cache
+
+    def eval_host(self, phase, smooth_pix=0.0):
+        """[..., D] referenced phases -> float32 [..., 4, ny, nx] (gather +
+        optional Gaussian smoothing) on the GPU."""
+        import torch
+        dev, lab = self._device()
+        phase = np.ascontiguousarray(phase, np.float64)
+        lead = phase.shape[:-1]
+        D = phase.shape[-1]
+        ny, nx = self.data_rasertize_template.shape
+        ph = torch.from_numpy(phase.reshape(-1, D)).to(dev)
+        S = ph.shape[0]
+        out = torch.empty((S, 4, ny, nx), dtype=torch.float32, device=dev)
+        ctx = get_context(self.device)
+        with torch.cuda.device(dev):
+            ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+            ctx.tess_fill(lab, nx, ny, ph, D, S, out, smooth_pix=smooth_pix,
+                          flags=SF_EVAL_NAN_SCRUB)
+        return out.cpu().numpy().reshape(lead + (4, ny, nx))
+
+    def make_matrix(self, t_start_index, t_stop_index, freq_ind, stat_ind,
+                    cellsize_deg, out_dir, ncpu):
+        """(t_stop - t_start, 4, ny, nx) (voronoi_screen.py:132-216)."""
+        del ncpu
+        if self.data_rasertize_template is None:
+            self.make_rasertize_template(cellsize_deg, out_dir)
+        ph = self.vals_ph[t_start_index:t_stop_index, freq_ind, stat_ind, :]
+        return self.eval_host(ph).astype(np.float64)
+
+    def write(self, out_dir, cellsize_deg, smooth_pix=0, ncpu=0):
+        if self.data_rasertize_template is None:
+            self.make_rasertize_template(cellsize_deg, out_dir)
+        return super().write(out_dir, cellsize_deg, smooth_pix=smooth_pix, ncpu=ncpu)
+
+    def write_chunk(self, writer, g_start, g_stop, cellsize_deg, smooth_pix,
+                    max_batch_bytes=2 << 30):
+        ny, nx = self.data_rasertize_template.shape
+        n_f, n_a = self.vals_ph.shape[1], self.vals_ph.shape[2]
+        rows = max(1, int(max_batch_bytes // (n_f * n_a * 16 * nx * ny)))
+        for t0 in range(g_start, g_stop, rows):
+            t1 = min(g_stop, t0 + rows)
+            writer.write(self.eval_host(self.vals_ph[t0:t1], smooth_pix))

@@ -1,0 +1,151 @@
+"""Tessellated (Voronoi) path: host template vs the oracle restatement and the
+reference's anchors (CPU), fused gather + Gaussian kernel vs the oracle /
+scipy.ndimage and the reference test criterion end to end (GPU).
+
+Parity status: the reference's own tessellated path needs shapely, absent
+from every interpreter here, so no golden raster exists; labels are pinned by
+the reference test's patch-pixel criterion and the survey probe count (5 of
+289 pixels differ from the nearest-direction map on the fixture).
+"""
+
+import os
+
+import numpy as np
+import pytest
+
+from conftest import FIELD, GOLDEN, load_golden
+from oracle import voronoi as ov
+from ska_sdp_screen_fitting_amd.voronoi_screen import (gaussian_weights,
+                                                       read_patch_positions,
+                                                       tessellation_template)
+
+SKY = os.path.join(GOLDEN, "skymodel.txt")
+
+
+def fixture_patches():
+    g = load_golden("fixture_kl")
+    pos = read_patch_positions(SKY)
+    dirs = [str(d) for d in g["dir_names"]]
+    return g, np.array([pos[d.strip("[]")] for d in dirs])
+
+
+def test_patch_positions_vs_astropy():
+    g, radec = fixture_patches()
+    np.testing.assert_allclose(radec, g["radec_patch"], rtol=0, atol=1e-10)
+    pos_o = ov.patch_positions(SKY)
+    for k, v in read_patch_positions(SKY).items():
+        np.testing.assert_allclose(v, pos_o[k], atol=1e-12)
+
+
+@pytest.mark.parametrize("cell", [0.2, 0.1, 0.05])
+def test_template_matches_oracle(cell):
+    _, radec = fixture_patches()
+    lab, xy = tessellation_template(radec, FIELD["rad"], FIELD["dec"],
+                                    FIELD["width"], cell)
+    lab_o, xy_o = ov.label_raster(radec[:, 0], radec[:, 1], FIELD["rad"],
+                                  FIELD["dec"], FIELD["width"], cell)
+    np.testing.assert_allclose(xy, xy_o, atol=1e-9)
+    np.testing.assert_array_equal(lab, lab_o)
+
+
+def test_template_anchors():
+    g, radec = fixture_patches()
+    lab, xy = tessellation_template(radec, FIELD["rad"], FIELD["dec"],
+                                    FIELD["width"], 0.2)
+    n = lab.shape[0]
+    assert n == 17 and lab.min() == 1 and lab.max() == 7
+    # patch pixels (via the cube's SIN WCS, golden from astropy) own their label
+    px, py = g["patch_pix17"]
+    for k in range(len(px)):
+        c, r = int(np.round(px[k])), int(np.round(py[k]))
+        if 0 <= r < n and 0 <= c < n:
+            assert lab[r, c] == k + 1
+    # survey probe: 5 of 289 pixels differ from the nearest-direction map
+    yy, xx = np.mgrid[0:n, 0:n]
+    near = ((xx[..., None] - xy[:, 0]) ** 2 + (yy[..., None] - xy[:, 1]) ** 2).argmin(-1) + 1
+    assert int((near != lab).sum()) == 5
+
+
+@pytest.mark.parametrize("sigma", [0.5, 1.3, 4.2])
+def test_gaussian_weights_match_scipy(sigma):
+    from scipy.ndimage import _filters
+    r, w = gaussian_weights(sigma)
+    np.testing.assert_array_equal(w, _filters._gaussian_kernel1d(sigma, 0, r)[::-1])
+
+
+# ----------------------------------------------------------------- GPU ----
+def _tess_gpu(lab, phase, smooth):
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from ska_sdp_screen_fitting_amd import get_context
+    dev = torch.device("cuda", 0)
+    ctx = get_context(0)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    ny, nx = lab.shape
+    S, D = phase.shape
+    lab_d = torch.from_numpy(np.ascontiguousarray(lab, np.int32)).to(dev)
+    ph_d = torch.from_numpy(np.ascontiguousarray(phase)).to(dev)
+    out = torch.full((S, 4, ny, nx), -5.0, dtype=torch.float32, device=dev)
+    ctx.tess_fill(lab_d, nx, ny, ph_d, D, S, out, smooth_pix=smooth)
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cell,smooth", [(0.2, 0.0), (0.2, 0.5), (0.05, 1.3),
+                                         (0.02602, 4.0)])
+def test_tess_kernel_vs_oracle(cell, smooth):
+    g, radec = fixture_patches()
+    lab, _ = tessellation_template(radec, FIELD["rad"], FIELD["dec"],
+                                   FIELD["width"], cell)
+    ref = int(g["ref_ant"])
+    ph = (g["val"] - g["val"][:, :, ref:ref + 1, :])[:, 3].reshape(-1, 7)[:150]
+    got = _tess_gpu(lab, ph, smooth)
+    want = ov.gather_planes(lab, ph)
+    if smooth > 0:
+        want = ov.smooth(want, smooth)
+        np.testing.assert_allclose(got, want, rtol=0, atol=1e-6)
+    else:
+        # fp64 cos/sin cast once to fp32: at most 1 ulp from numpy's libm
+        assert np.max(np.abs(got.view(np.int32) - want.view(np.int32))) <= 1
+
+
+@pytest.mark.gpu
+def test_make_aterm_image_fixture_tessellated(tmp_path):
+    """tests/test_fit_screens.py::test_fit_voronoi_screens (abs(), 1e-4)."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from ska_sdp_screen_fitting_amd import fits as sffits
+    from ska_sdp_screen_fitting_amd.make_aterm_images import make_aterm_image
+    g = load_golden("fixture_kl")
+    outroot = str(tmp_path / "tessellated")
+    make_aterm_image(os.path.join(GOLDEN, "fixture_kl.npz"), soltabname="phase000",
+                     screen_type="tessellated", outroot=outroot,
+                     bounds_deg=[124.565, 66.165, 127.895, 62.835],
+                     bounds_mid_deg=[126.23, 64.50], skymodel=SKY,
+                     solsetname="sol000", padding_fraction=0, cellsize_deg=0.2,
+                     smooth_deg=0.1, ncpu=0)
+    for f in ("tessellated_0.fits", "tessellated_template.fits", "tessellated.txt"):
+        assert os.path.isfile(str(tmp_path / f)), f
+    hdr, cube = sffits.read_cube(outroot + "_0.fits")
+    assert cube.shape == (20, 12, 62, 4, 17, 17)
+    ph = np.asarray(g["val"])
+    corr = ph - ph[:, :, 0:1, :]
+    px, py = g["patch_pix17"]
+    n_in = 0
+    for i in range(len(px)):
+        col, row = int(np.round(px[i])), int(np.round(py[i]))
+        if 0 <= row < 17 and 0 <= col < 17:
+            n_in += 1
+            for p, fn in ((0, np.cos), (1, np.sin), (2, np.cos), (3, np.sin)):
+                err = np.abs(cube[:, :, :, p, row, col] - fn(corr[..., i]))
+                assert np.all(err < 1e-4), (i, p, err.max())
+    assert n_in >= 5
+    # the whole cube vs the oracle (gather + scipy gaussian, smooth 0.5 px)
+    _, radec = fixture_patches()
+    lab, _ = tessellation_template(radec, FIELD["rad"], FIELD["dec"],
+                                   FIELD["width"], 0.2)
+    want = ov.smooth(ov.gather_planes(lab, corr), 0.5)
+    np.testing.assert_allclose(cube, want, rtol=0, atol=1e-6)
