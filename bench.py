@@ -50,6 +50,8 @@ def parse():
                     help="fp64 sincos epilogue (default: fp64 range reduction "
                          "+ fp32 sincos, |err| <= 3e-7)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-fits", action="store_true",
+                    help="skip the FITS-cube wall-clock leg (configs 1-2)")
     ap.add_argument("--cpu-workers", type=int, default=16)
     ap.add_argument("--eval-only", action="store_true",
                     help="time only sf_kl_eval (profiling)")
@@ -124,6 +126,27 @@ def cpu_baseline(sol, setup, n_workers, slots_fit=64, slots_eval=192):
                    f"fit {t_fit / n_fit * 1e3:.3f} ms/slot/core, eval "
                    f"{t_ev / n_ev * 1e3:.1f} ms/slot/core"),
     }
+
+
+def fits_wallclock():
+    """FITS-cube wall-clock of make_aterm_image on the reference fixture:
+    config 1 (tessellated 17^2, smooth 0.1 deg) and config 2 (KL 128^2);
+    fit + evaluation + FITS write, host I/O included (second run of each,
+    i.e. with the device context warm)."""
+    import tempfile
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import fits_wallclock as fw
+    res = {}
+    for name in ("config1", "config2"):
+        best = None
+        for _ in range(2):
+            with tempfile.TemporaryDirectory() as d:
+                r = fw.run(name, d)
+            best = r if best is None or r["wall_s"] < best["wall_s"] else best
+        res[name] = {"wall_s": best["wall_s"], "fits_bytes": best["fits_bytes"],
+                     "screen_type": best["screen_type"],
+                     "grid": 17 if name == "config1" else 128}
+    return res
 
 
 def main():
@@ -281,6 +304,8 @@ def main():
             "fit_stats": fit_stats,
             "check": {"max_abs_cos2_plus_sin2_minus_1": unit_err},
         }
+        if not args.no_fits:
+            line["fits_wallclock"] = fits_wallclock()
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(
                 sol, setup, max(1, min(args.cpu_workers, os.cpu_count() or 1)))

@@ -65,6 +65,8 @@ extern "C" {
 #define SF_EVAL_FAST_SINCOS (1u << 8) /* fp64 range reduction + fp32 sincos
                                          (|err| <= 3e-7) instead of fp64 sincos */
 #define SF_EVAL_NT_STORES (1u << 9) /* non-temporal (streaming) cube stores */
+#define SF_EVAL_BIG_ENDIAN (1u << 10) /* store big-endian float32 (the FITS
+                                         byte order), for direct file writes */
 
 typedef struct sf_ctx sf_ctx;
 

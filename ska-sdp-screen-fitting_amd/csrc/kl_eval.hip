@@ -91,6 +91,10 @@ __device__ __forceinline__ void jones_sincos(double ph, float& s, float& c) {
 
 typedef float v4f __attribute__((ext_vector_type(4)));
 
+__device__ __forceinline__ float bswapf(float x) {
+  return __uint_as_float(__builtin_bswap32(__float_as_uint(x)));
+}
+
 template <bool NT>
 __device__ __forceinline__ void store4(float* p, v4f v) {
   if (NT) __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(p));
@@ -129,6 +133,7 @@ __global__ __launch_bounds__(256, SF_EVAL_MIN_WAVES) void kl_eval_kernel(
       bf[kk][t] = cfrag[((wpb * KS + kk) * kTiles + t) * 64 + l];
 
   const bool scrub = flags & SF_EVAL_NAN_SCRUB;
+  const bool be = flags & SF_EVAL_BIG_ENDIAN;
   const int64_t slot_base = sc * (int64_t)chunk_groups * 16;
   for (int g = 0; g < chunk_groups; ++g) {
     const int64_t s0 = slot_base + (int64_t)g * 16;
@@ -162,6 +167,10 @@ __global__ __launch_bounds__(256, SF_EVAL_MIN_WAVES) void kl_eval_kernel(
         if (scrub) {
           if (isnan(cv[t])) cv[t] = 1.0f;
           if (isnan(sv[t])) sv[t] = 0.0f;
+        }
+        if (be) {
+          cv[t] = bswapf(cv[t]);
+          sv[t] = bswapf(sv[t]);
         }
       }
       float* o = out + ((s % ring) * 4) * P + p0;

@@ -112,6 +112,8 @@ __global__ __launch_bounds__(256) void kl_tess_kernel(
       for (int p = 0; p < 4; ++p) {
         float x = v[p];
         if (scrub && isnan(x)) x = (p & 1) ? 0.0f : 1.0f;
+        if (flags & SF_EVAL_BIG_ENDIAN)
+          x = __uint_as_float(__builtin_bswap32(__float_as_uint(x)));
         o[p * P] = x;
       }
     }

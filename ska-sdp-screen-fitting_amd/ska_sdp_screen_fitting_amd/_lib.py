@@ -18,6 +18,7 @@ SF_SCREEN_TEC = 1
 SF_EVAL_NAN_SCRUB = 1
 SF_EVAL_FAST_SINCOS = 1 << 8
 SF_EVAL_NT_STORES = 1 << 9
+SF_EVAL_BIG_ENDIAN = 1 << 10
 SF_MAX_DIR = 60
 SF_OPT_FIT_GENERAL = 1
 

@@ -94,6 +94,12 @@ class CubeWriter:
         self.fh.write(a.tobytes())
         self.written += a.nbytes
 
+    def write_raw(self, buf):
+        """Append bytes that are already big-endian float32 (device stores
+        with SF_EVAL_BIG_ENDIAN)."""
+        self.fh.write(buf)
+        self.written += len(buf)
+
     def close(self):
         if self.fh is None:
             return

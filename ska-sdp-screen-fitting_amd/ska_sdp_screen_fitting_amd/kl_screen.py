@@ -14,8 +14,8 @@ import numpy as np
 
 from . import geometry
 from . import stationscreen
-from ._lib import (SF_EVAL_FAST_SINCOS, SF_EVAL_NAN_SCRUB, SF_EVAL_NT_STORES,
-                   get_context)
+from ._lib import (SF_EVAL_BIG_ENDIAN, SF_EVAL_FAST_SINCOS, SF_EVAL_NAN_SCRUB,
+                   SF_EVAL_NT_STORES, get_context)
 from .h5parm import H5parm, get_reference_station
 from .screen import Screen
 
@@ -159,14 +159,29 @@ class KLScreen(Screen):
         return self.evaluator(cellsize_deg).eval_host(coef).astype(np.float64)
 
     def write_chunk(self, writer, g_start, g_stop, cellsize_deg, smooth_pix,
-                    max_batch_bytes=2 << 30):
-        """All (freq, station) screens of times [g_start, g_stop) in device
-        batches of whole time rows, streamed to the FITS writer."""
+                    max_batch_bytes=1 << 30):
+        """All (freq, station) screens of times [g_start, g_stop): device
+        batches of whole time rows in FITS byte order, streamed through
+        pinned buffers to the file while the next batch is evaluated."""
+        from .streaming import PinnedPipeline
+        torch = __import__("torch")
         ev = self.evaluator(cellsize_deg)
         vals = np.asarray(self.vals_ph)
-        n_f, n_a = vals.shape[1], vals.shape[2]
-        row_bytes = n_f * n_a * 4 * ev.nx * ev.ny * 4
-        rows = max(1, int(max_batch_bytes // max(row_bytes, 1)))
-        for t0 in range(g_start, g_stop, rows):
-            t1 = min(g_stop, t0 + rows)
-            writer.write(ev.eval_host(vals[t0:t1]))
+        n_f, n_a, D = vals.shape[1], vals.shape[2], vals.shape[3]
+        per_slot = 16 * ev.nx * ev.ny
+        row_bytes = n_f * n_a * per_slot
+        rows = max(1, int(max_batch_bytes // row_bytes))
+        rows = min(rows, g_stop - g_start)
+        coef = torch.from_numpy(np.ascontiguousarray(
+            vals[g_start:g_stop].reshape(-1, D), np.float64)).to(ev.dev)
+        pipe = PinnedPipeline(torch, ev.dev, rows * row_bytes)
+        try:
+            for t0 in range(g_start, g_stop, rows):
+                t1 = min(g_stop, t0 + rows)
+                s0, s1 = (t0 - g_start) * n_f * n_a, (t1 - g_start) * n_f * n_a
+                slot, buf = pipe.device_buffer((s1 - s0) * per_slot)
+                out = buf.view(torch.float32).view(s1 - s0, 4, ev.ny, ev.nx)
+                ev.eval_device(coef[s0:s1], out, DEFAULT_FLAGS | SF_EVAL_BIG_ENDIAN)
+                pipe.submit(slot, (s1 - s0) * per_slot, writer)
+        finally:
+            pipe.close()

@@ -19,7 +19,7 @@ from PIL import Image, ImageDraw
 from scipy.spatial import Voronoi
 
 from . import fits, geometry
-from ._lib import SF_EVAL_NAN_SCRUB, get_context
+from ._lib import SF_EVAL_BIG_ENDIAN, SF_EVAL_NAN_SCRUB, get_context
 from .h5parm import H5parm, get_reference_station
 from .screen import Screen
 
@@ -199,23 +199,31 @@ class VoronoiScreen(Screen):
             self._dev_cache = (dev, lab)
         return self._dev_cache
 
+    def eval_device(self, ph_dev, out_dev, smooth_pix=0.0,
+                    flags=SF_EVAL_NAN_SCRUB):
+        """device [S, D] referenced phases -> device [S, 4, ny, nx]."""
+        import torch
+        dev, lab = self._device()
+        ny, nx = self.data_rasertize_template.shape
+        S, D = ph_dev.shape
+        ctx = get_context(self.device)
+        with torch.cuda.device(dev):
+            ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+            ctx.tess_fill(lab, nx, ny, ph_dev, D, S, out_dev,
+                          smooth_pix=smooth_pix, flags=flags)
+        return out_dev
+
     def eval_host(self, phase, smooth_pix=0.0):
         """[..., D] referenced phases -> float32 [..., 4, ny, nx] (gather +
         optional Gaussian smoothing) on the GPU."""
         import torch
-        dev, lab = self._device()
+        dev, _ = self._device()
         phase = np.ascontiguousarray(phase, np.float64)
         lead = phase.shape[:-1]
-        D = phase.shape[-1]
         ny, nx = self.data_rasertize_template.shape
-        ph = torch.from_numpy(phase.reshape(-1, D)).to(dev)
-        S = ph.shape[0]
-        out = torch.empty((S, 4, ny, nx), dtype=torch.float32, device=dev)
-        ctx = get_context(self.device)
-        with torch.cuda.device(dev):
-            ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
-            ctx.tess_fill(lab, nx, ny, ph, D, S, out, smooth_pix=smooth_pix,
-                          flags=SF_EVAL_NAN_SCRUB)
+        ph = torch.from_numpy(phase.reshape(-1, phase.shape[-1])).to(dev)
+        out = torch.empty((ph.shape[0], 4, ny, nx), dtype=torch.float32, device=dev)
+        self.eval_device(ph, out, smooth_pix)
         return out.cpu().numpy().reshape(lead + (4, ny, nx))
 
     def make_matrix(self, t_start_index, t_stop_index, freq_ind, stat_ind,
@@ -233,10 +241,28 @@ class VoronoiScreen(Screen):
         return super().write(out_dir, cellsize_deg, smooth_pix=smooth_pix, ncpu=ncpu)
 
     def write_chunk(self, writer, g_start, g_stop, cellsize_deg, smooth_pix,
-                    max_batch_bytes=2 << 30):
+                    max_batch_bytes=1 << 30):
+        """Gather + smoothing of times [g_start, g_stop) in FITS byte order,
+        streamed through pinned buffers (see streaming.py)."""
+        import torch
+        from .streaming import PinnedPipeline
+        dev, _ = self._device()
         ny, nx = self.data_rasertize_template.shape
-        n_f, n_a = self.vals_ph.shape[1], self.vals_ph.shape[2]
-        rows = max(1, int(max_batch_bytes // (n_f * n_a * 16 * nx * ny)))
-        for t0 in range(g_start, g_stop, rows):
-            t1 = min(g_stop, t0 + rows)
-            writer.write(self.eval_host(self.vals_ph[t0:t1], smooth_pix))
+        n_f, n_a, D = self.vals_ph.shape[1:]
+        per_slot = 16 * nx * ny
+        row_bytes = n_f * n_a * per_slot
+        rows = min(max(1, int(max_batch_bytes // row_bytes)), g_stop - g_start)
+        ph = torch.from_numpy(np.ascontiguousarray(
+            self.vals_ph[g_start:g_stop].reshape(-1, D), np.float64)).to(dev)
+        pipe = PinnedPipeline(torch, dev, rows * row_bytes)
+        try:
+            for t0 in range(g_start, g_stop, rows):
+                t1 = min(g_stop, t0 + rows)
+                s0, s1 = (t0 - g_start) * n_f * n_a, (t1 - g_start) * n_f * n_a
+                slot, buf = pipe.device_buffer((s1 - s0) * per_slot)
+                out = buf.view(torch.float32).view(s1 - s0, 4, ny, nx)
+                self.eval_device(ph[s0:s1], out, smooth_pix,
+                                 SF_EVAL_NAN_SCRUB | SF_EVAL_BIG_ENDIAN)
+                pipe.submit(slot, (s1 - s0) * per_slot, writer)
+        finally:
+            pipe.close()
