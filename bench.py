@@ -34,7 +34,7 @@ WORKLOADS = {
     # name: (ant per GPU, times, freqs, dirs, grid side, cellsize)
     "config3": (64, 100, 16, 20, 256, 0.01301),
     "config2-shape": (62, 20, 12, 7, 128, 0.02602),
-    "config5-shape": (16, 50, 4, 50, 512, 0.006505),
+    "config5-shape": (64, 100, 4, 50, 512, 0.006505),
 }
 
 

@@ -52,7 +52,8 @@ __global__ __launch_bounds__(64) void kl_basis_kernel(
   double* a = smem;
   double* v = a + D * ld;
   double2* cs = reinterpret_cast<double2*>(v + D * ld);
-  int* perm = reinterpret_cast<int*>(cs + 64);
+  int2* pr = reinterpret_cast<int2*>(cs + 64);      // 64 int2 + 64 int
+  int* perm = reinterpret_cast<int*>(pr + 96);
   const int i = lane();
   const double r0sq = r0 * r0, hb = beta / 2.0;
   if (i < D) {
@@ -63,7 +64,7 @@ __global__ __launch_bounds__(64) void kl_basis_kernel(
     }
   }
   lds_sync();
-  wave_jacobi(a, v, cs, D, ld, kMaxSweeps);
+  wave_jacobi(a, v, cs, pr, D, ld, kMaxSweeps);
   wave_eig_order(a, D, ld, perm);
   if (i < D) {
     for (int r = 0; r < D; ++r) u_out[i * D + r] = v[i * ld + perm[r]];
@@ -124,6 +125,7 @@ struct FitLds {
   int* idx;      // [64] subset -> direction
   int* perm;     // [64] rank -> column of V
   double2* cs;   // [64] Jacobi rotations
+  int2* pr;      // [64] + 64 int: Jacobi round pairs / partners
 };
 
 __host__ __device__ inline size_t fit_shared_bytes(int D) {
@@ -131,7 +133,8 @@ __host__ __device__ inline size_t fit_shared_bytes(int D) {
 }
 __host__ __device__ inline size_t fit_wave_bytes(int D) {
   return (size_t)(3 * D * odd_ld(D) + 64 + 6 * 64) * sizeof(double) +
-         (size_t)(64 + 64) * sizeof(int) + 64 * sizeof(double2);
+         (size_t)(64 + 64) * sizeof(int) + 64 * sizeof(double2) +
+         96 * sizeof(int2);
 }
 
 struct SubsetState {
@@ -166,7 +169,7 @@ __device__ void setup_subset(const FitLds& L, int D, int ld, double w_d,
     for (int q = 0; q < n; ++q) L.M1[d * ld + q] = L.C[r * ld + L.idx[q]];
   }
   lds_sync();
-  wave_jacobi(L.M1, L.V, L.cs, n, ld, kMaxSweeps);
+  wave_jacobi(L.M1, L.V, L.cs, L.pr, n, ld, kMaxSweeps);
   wave_eig_order(L.M1, n, ld, L.perm);
   if (d < n) {
     const int m = L.perm[d];
@@ -293,7 +296,7 @@ __device__ void fit_screen(const FitLds& L, const SubsetState& st, int D,
     if (st.wmin > kPinvAtol * (1.0 + 1e-9)) {
       wave_cholesky_solve2(L.M2, K, ld, a1, a2);
     } else {
-      wave_jacobi(L.M2, L.M1, L.cs, K, ld, kMaxSweeps);
+      wave_jacobi(L.M2, L.M1, L.cs, L.pr, K, ld, kMaxSweeps);
       if (lp < K) {
         v0[lp] = g1;
         v1[lp] = g2;
@@ -413,6 +416,7 @@ __global__ __launch_bounds__(256) void kl_fit_general_kernel(
   L.idx = reinterpret_cast<int*>(L.vec + 6 * 64);
   L.perm = L.idx + 64;
   L.cs = reinterpret_cast<double2*>(L.perm + 64);
+  L.pr = reinterpret_cast<int2*>(L.cs + 64);
   // shared basis -> LDS
   for (int e = threadIdx.x; e < D * D; e += blockDim.x) {
     const int r = e / D, c = e % D;
@@ -553,7 +557,7 @@ int launch_basis(sf_ctx* ctx) {
   const int D = ctx->D;
   const int ld = odd_ld(D);
   const size_t shm = (size_t)2 * D * ld * sizeof(double) + 64 * sizeof(double2) +
-                     64 * sizeof(int);
+                     96 * sizeof(int2) + 64 * sizeof(int);
   hipLaunchKernelGGL(kl_basis_kernel, dim3(1), dim3(64), shm, ctx->stream,
                      ctx->d_pp, D, ctx->r0, ctx->beta, ctx->d_c, ctx->d_pinv,
                      ctx->d_u, ctx->d_eig);

@@ -146,7 +146,8 @@ __global__ __launch_bounds__(64) void kl_subset_eig_kernel(
   double* a = smem;
   double* v = a + D * ld;
   double2* cs = reinterpret_cast<double2*>(v + D * ld);
-  int* perm = reinterpret_cast<int*>(cs + 64);
+  int2* pr = reinterpret_cast<int2*>(cs + 64);  // 64 int2 + 64 int
+  int* perm = reinterpret_cast<int*>(pr + 96);
   int* idx = perm + 64;
   const int first = counters[1];
   const int last = min(counters[0], pool_cap);
@@ -166,7 +167,7 @@ __global__ __launch_bounds__(64) void kl_subset_eig_kernel(
       for (int q = 0; q < n; ++q) a[l * ld + q] = g_c[r * D + idx[q]];
     }
     lds_sync();
-    wave_jacobi(a, v, cs, n, ld, 40);
+    wave_jacobi(a, v, cs, pr, n, ld, 40);
     wave_eig_order(a, n, ld, perm);
     double* e = pool + (size_t)id * (D * D + D);
     if (l < n) {
@@ -640,7 +641,8 @@ static int number_and_decompose(sf_ctx* ctx) {
   if (n_new > 0) {
     const int D = ctx->D;
     const size_t shm = (size_t)2 * D * ldo(D) * sizeof(double) +
-                       64 * sizeof(double2) + 128 * sizeof(int);
+                       64 * sizeof(double2) + 96 * sizeof(int2) +
+                       128 * sizeof(int);
     if (shm > 64 * 1024)
       SF_HIP(hipFuncSetAttribute(
           reinterpret_cast<const void*>(&kl_subset_eig_kernel),

@@ -52,18 +52,24 @@ __device__ __forceinline__ int rr_partner(int i, int r, int m) {
 
 // Cyclic Jacobi eigen-decomposition of the symmetric n x n matrix `a`
 // (in place; on exit diag(a) = eigenvalues) accumulating the eigenvectors in
-// the columns of `v`.  `cs` is LDS scratch of 64 double2 for the rotations of
-// one round.  Each round applies n/2 disjoint rotations A <- J^T A J at once;
-// the update of element (i, j) reads A_ij, A_{pi,j}, A_{i,pj}, A_{pi,pj}
-// (pi, pj = round partners), so every read of a column pair happens before
-// any write to it (lds_sync between the two phases).
-__device__ inline int wave_jacobi(double* a, double* v, double2* cs, int n,
-                                  int ld, int max_sweeps) {
+// the columns of `v`.  `cs` is LDS scratch of 64 double2 (the rotation of
+// each row/column this round), `pr` LDS scratch of 64 int2 (the round's
+// column pairs) and 64 ints (each row's partner).
+// Each round applies the n/2 disjoint rotations of a round-robin pairing at
+// once, A <- J^T A J, V <- V J: lane i owns row i; the element (i, j) update
+// reads A_ij, A_i,pj, A_pi,j, A_pi,pj, so a chunk of column pairs is read by
+// the whole wave before any of it is written (lds_sync between).  The loop
+// over column pairs is branch-free (an unpaired column is paired with
+// itself under the identity rotation), so the reads of a chunk issue
+// back-to-back.
+__device__ inline int wave_jacobi(double* a, double* v, double2* cs, int2* pr,
+                                  int n, int ld, int max_sweeps) {
 #pragma clang fp contract(off)
   const int i = lane();
   const bool own = i < n;
   const int m = n + (n & 1);
-  // V = I
+  const int npairs = m / 2;
+  int* part = reinterpret_cast<int*>(pr + 64);
   for (int j = 0; j < n; ++j)
     if (own) v[i * ld + j] = (i == j) ? 1.0 : 0.0;
   lds_sync();
@@ -83,14 +89,27 @@ __device__ inline int wave_jacobi(double* a, double* v, double2* cs, int n,
     // sweep after ~1e-7; a stricter test never triggers for n >= 10)
     if (!(off > 1e-26 * (off + dia))) break;
     for (int r = 0; r < m - 1; ++r) {
-      // rotation of the pair containing lane i, computed by its smaller member
-      const int pi = (i < m) ? rr_partner(i, r, m) : i;
-      if (own && pi < n && i < pi) {
-        const double app = a[i * ld + i];
-        const double aqq = a[pi * ld + pi];
-        const double apq = a[i * ld + pi];
+      // pair k of round r: (m-1, r) for k = 0, else (r+k, r-k) mod (m-1);
+      // a pair with the dummy player n (n odd) becomes (j, j)
+      if (i < npairs) {
+        int p, q;
+        if (i == 0) {
+          p = r;
+          q = m - 1;
+        } else {
+          p = r + i;
+          if (p >= m - 1) p -= m - 1;
+          q = r - i;
+          if (q < 0) q += m - 1;
+        }
+        if (q >= n) q = p;
+        if (p >= n) p = q;
+        if (p > q) { const int t = p; p = q; q = t; }
         double c = 1.0, s = 0.0;
-        if (apq != 0.0) {
+        const double apq = a[p * ld + q];
+        if (p != q && apq != 0.0) {
+          const double app = a[p * ld + p];
+          const double aqq = a[q * ld + q];
           const double tau = (aqq - app) / (2.0 * apq);
           double t;
           if (fabs(tau) > 1e150) {
@@ -102,68 +121,58 @@ __device__ inline int wave_jacobi(double* a, double* v, double2* cs, int n,
           c = 1.0 / sqrt(1.0 + t * t);
           s = t * c;
         }
-        cs[i] = make_double2(c, -s);  // row/col of p: x_p' = c x_p - s x_q
-        cs[pi] = make_double2(c, s);  // row/col of q: x_q' = c x_q + s x_p
-      } else if (own && pi >= n) {
-        cs[i] = make_double2(1.0, 0.0);
+        pr[i] = make_int2(p, q);
+        cs[p] = make_double2(c, -s);  // row/col p: x_p' = c x_p - s x_q
+        part[p] = q;
+        if (q != p) {
+          cs[q] = make_double2(c, s);  // row/col q: x_q' = c x_q + s x_p
+          part[q] = p;
+        }
       }
       lds_sync();
       const double2 ri = own ? cs[i] : make_double2(1.0, 0.0);
-      const int pir = (own && pi < n) ? pi : i;
-      // A'' = J^T A J, processed in column pairs (j, pj), chunked so that the
-      // reads of a chunk precede its writes for the whole wave.
-      constexpr int CH = 8;
-      for (int j0 = 0; j0 < n; j0 += CH) {
+      const int pir = own ? part[i] : 0;
+      constexpr int CH = 4;  // column pairs per chunk
+      for (int k0 = 0; k0 < npairs; k0 += CH) {
         double na[CH], nb[CH], nv[CH], nw[CH];
-        int jj[CH], pjj[CH];
+        int jj[CH], qq[CH];
 #pragma unroll
         for (int u = 0; u < CH; ++u) {
-          const int j = j0 + u;
-          int pj = (j < n) ? rr_partner(j, r, m) : n;
+          const int k = min(k0 + u, npairs - 1);
+          const int2 jq = pr[k];
+          const int j = jq.x, pj = jq.y;
           jj[u] = j;
-          pjj[u] = pj;
-          na[u] = nb[u] = nv[u] = nw[u] = 0.0;
-          if (own && j < n && (pj >= n || j < pj)) {
-            const double2 rj = cs[j];
-            if (pj >= n) {
-              // column j unpaired this round
-              const double aij = a[i * ld + j];
-              const double apj = a[pir * ld + j];
-              na[u] = ri.x * aij + ri.y * apj;
-              nv[u] = v[i * ld + j];
-            } else {
-              const double2 rq = cs[pj];
-              const double aij = a[i * ld + j];
-              const double aiq = a[i * ld + pj];
-              const double apj = a[pir * ld + j];
-              const double apq = a[pir * ld + pj];
-              // row rotation then column rotation, summed symmetrically
-              const double r_j = ri.x * aij + ri.y * apj;   // R_ij
-              const double r_q = ri.x * aiq + ri.y * apq;   // R_i,pj
-              na[u] = rj.x * r_j + rj.y * r_q;              // A''_ij
-              nb[u] = rq.x * r_q + rq.y * r_j;              // A''_i,pj
-              const double vij = v[i * ld + j];
-              const double viq = v[i * ld + pj];
-              nv[u] = rj.x * vij + rj.y * viq;
-              nw[u] = rq.x * viq + rq.y * vij;
+          qq[u] = pj;
+          const double2 rj = cs[j];
+          const double2 rq = cs[pj];
+          const double aij = a[i * ld + j];
+          const double aiq = a[i * ld + pj];
+          const double apj = a[pir * ld + j];
+          const double apq = a[pir * ld + pj];
+          const double vij = v[i * ld + j];
+          const double viq = v[i * ld + pj];
+          // row rotation then column rotation, summed symmetrically
+          const double r_j = ri.x * aij + ri.y * apj;   // R_ij
+          const double r_q = ri.x * aiq + ri.y * apq;   // R_i,pj
+          na[u] = rj.x * r_j + rj.y * r_q;              // A''_ij
+          nb[u] = rq.x * r_q + rq.y * r_j;              // A''_i,pj
+          nv[u] = rj.x * vij + rj.y * viq;
+          nw[u] = rq.x * viq + rq.y * vij;
+        }
+        lds_sync();
+        if (own) {
+#pragma unroll
+          for (int u = 0; u < CH; ++u) {
+            a[i * ld + jj[u]] = na[u];
+            v[i * ld + jj[u]] = nv[u];
+            if (qq[u] != jj[u]) {
+              a[i * ld + qq[u]] = nb[u];
+              v[i * ld + qq[u]] = nw[u];
             }
           }
         }
         lds_sync();
-#pragma unroll
-        for (int u = 0; u < CH; ++u) {
-          const int j = jj[u], pj = pjj[u];
-          if (own && j < n && (pj >= n || j < pj)) {
-            a[i * ld + j] = na[u];
-            v[i * ld + j] = nv[u];
-            if (pj < n) {
-              a[i * ld + pj] = nb[u];
-              v[i * ld + pj] = nw[u];
-            }
-          }
-        }
       }
-      lds_sync();
     }
   }
   return sweep;
