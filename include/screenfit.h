@@ -59,6 +59,7 @@ extern "C" {
 /* screen types of stationscreen.run (stationscreen.py:922-928) */
 #define SF_SCREEN_PHASE 0
 #define SF_SCREEN_TEC 1
+#define SF_SCREEN_AMPLITUDE 2 /* log10 fit; sigma per station block (Q6) */
 
 /* sf_kl_eval flags */
 #define SF_EVAL_NAN_SCRUB 1u /* NaN -> 1 (real planes), 0 (imag) (screen.py:368-378) */
@@ -72,7 +73,7 @@ typedef struct sf_ctx sf_ctx;
 
 /* Operator parameters of stationscreen.run (stationscreen.py:858-871). */
 typedef struct sf_fit_params {
-  int screen_type;  /* SF_SCREEN_PHASE or SF_SCREEN_TEC */
+  int screen_type;  /* SF_SCREEN_PHASE, _TEC or _AMPLITUDE */
   int niter;        /* outlier-flagging iterations (phase: 2) */
   double nsigma;    /* outlier threshold in circular sigmas (5.0) */
   int adjust_order; /* adapt the order toward reduced chi^2 ~ 1 (1) */
@@ -154,6 +155,15 @@ int sf_set_grid(sf_ctx* ctx, const double* x_host, int nx,
  */
 int sf_kl_eval(sf_ctx* ctx, const double* coef, int64_t S, float* out,
                int64_t ring_slots, unsigned flags);
+
+/*
+ * Gain screens (kl_screen.py:319-378): three KL screens on the same pixel
+ * basis -- phase and the XX / YY log10-amplitude screens -- written as
+ * (10^xx cos, 10^xx sin, 10^yy cos, 10^yy sin).  Device coef arrays [S][D].
+ */
+int sf_kl_eval_gain(sf_ctx* ctx, const double* coef_phase,
+                    const double* coef_xx, const double* coef_yy, int64_t S,
+                    float* out, int64_t ring_slots, unsigned flags);
 
 /*
  * Tessellated (Voronoi) screens: fill every pixel with the values of the

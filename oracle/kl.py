@@ -141,6 +141,8 @@ def fit_screen(phi, w, order, basis, screen_type="phase"):
         screen = np.arctan2(c @ im, c @ re)
     elif screen_type == "tec":
         screen = c @ project(phi[unfl])
+    elif screen_type == "amplitude":
+        screen = c @ project(np.log10(phi[unfl]))
     else:
         raise ValueError(screen_type)
     white = pinv_c @ screen
@@ -153,10 +155,16 @@ def fit_screen(phi, w, order, basis, screen_type="phase"):
             cval = -((d2 / basis.r_0 ** 2) ** (basis.beta / 2.0)) / 2.0
             screen_all[f] = cval @ white
         white_all = basis.pinv_c @ screen_all
-        resid_all = phi - screen_all
+        if screen_type == "amplitude":
+            resid_all = phi - 10 ** screen_all
+        else:
+            resid_all = phi - screen_all
     else:
         white_all = white
-        resid_all = phi - c @ white
+        if screen_type == "amplitude":
+            resid_all = phi - 10 ** (c @ white)
+        else:
+            resid_all = phi - c @ white
     return white_all, resid_all
 
 
@@ -319,3 +327,139 @@ def eval_planes(phase, amp_xx=None, amp_yy=None):
     if amp_xx is None:
         return np.stack([c, s, c, s], axis=-2)
     return np.stack([amp_xx * c, amp_xx * s, amp_yy * c, amp_yy * s], axis=-2)
+
+
+def process_station_block(vals, wts, order0, basis, screen_type, niter=2,
+                          nsigma=5.0, adjust_order=True):
+    """stationscreen.py:597-782 for a whole [D, T] station block (any screen
+    type; amplitude / tec flag with ONE sigma over the block, quirk Q6).
+    Returns (white [D, T], resid [D, T], w [D, T], orders [T])."""
+    d, t_n = vals.shape
+    screen = np.zeros((d, t_n))
+    resid = np.zeros((d, t_n))
+    order = np.full(t_n, float(order0))
+    station_order = float(order0)
+    w = np.asarray(wts, np.float32).copy()
+    for it in range(niter):
+        if it > 0:
+            if screen_type in ("phase", "tec"):
+                diff = resid.copy()
+            else:
+                diff = np.log10(vals) - np.log10(np.abs(vals - resid))
+            nonfl = np.where(w > 0.0)
+            if nonfl[0].size > 0:
+                if screen_type == "phase":
+                    r = normalize_phase(diff)
+                    rn = r.copy()
+                    rn[np.where(w == 0.0)] = np.nan
+                    std = nancircstd(rn, axis=0)
+                else:
+                    r = diff
+                    std = np.sqrt(np.average(r[nonfl] ** 2, weights=w[nonfl], axis=0))
+                with np.errstate(invalid="ignore"):
+                    w[np.where(np.abs(r) > nsigma * std)] = 0.0
+        norderiter = 4 if (adjust_order and it > 0) else 1
+        for t in range(t_n):
+            n_unfl = int(np.sum(w[:, t] > 0.0))
+            if n_unfl == 0:
+                continue
+            if order[t] > n_unfl - 1:
+                order[t] = n_unfl - 1
+            hit_upper = hit_lower = hit_upper2 = hit_lower2 = False
+            sign = 1.0
+            prev = 0.0
+            for oi in range(norderiter):
+                skip = False
+                if it > 0:
+                    if not adjust_order:
+                        break
+                    if oi == 0:
+                        skip = True
+                if not np.all(w[:, t] == 0.0) and not skip:
+                    wh, rs = fit_screen(vals[:, t], w[:, t], int(order[t]), basis,
+                                        screen_type)
+                    screen[:, t] = wh
+                    resid[:, t] = rs
+                if hit_lower2 or hit_upper2:
+                    break
+                if adjust_order and it > 0:
+                    if screen_type == "phase":
+                        redchi2 = circ_chi2(resid[:, t], w[:, t]) / (n_unfl - order[t])
+                    elif screen_type == "amplitude":
+                        sd = np.log10(vals[:, t]) - np.log10(np.abs(vals[:, t] - resid[:, t]))
+                        redchi2 = np.sum(np.square(sd) * w[:, t]) / (n_unfl - order[t])
+                    else:
+                        redchi2 = np.sum(np.square(resid[:, t]) * w[:, t]) / (n_unfl - order[t])
+                    if oi > 0:
+                        if redchi2 > 1.0 and prev < redchi2:
+                            sign *= -1
+                        if redchi2 < 1.0 and prev > redchi2:
+                            sign *= -1
+                    prev = redchi2
+                    factor = (n_unfl - order[t]) ** 0.2
+                    target = float(order[t]) - sign * factor * (1.0 - redchi2)
+                    target = max(station_order, target)
+                    target = min(int(round(target)), n_unfl - 1)
+                    if target <= 0:
+                        target = min(station_order, n_unfl - 1)
+                    if target == order[t]:
+                        break
+                    if target == n_unfl - 1:
+                        if hit_upper:
+                            hit_upper2 = True
+                        hit_upper = True
+                    if target == station_order:
+                        if hit_lower:
+                            hit_lower2 = True
+                        hit_lower = True
+                    order[t] = target
+    return screen, resid, w, order
+
+
+def run_amplitude(val, weight, pp, order, r_0=100.0, beta=5.0 / 3.0, niter=3,
+                  nsigma=5.0, adjust_order=True):
+    """stationscreen.run on an amplitude soltab [time, freq, ant, dir, pol] as
+    KLScreen.fit calls it (kl_screen.py:117-125: ref_ant=-1,
+    scale_order=False)."""
+    val = np.asarray(val, np.float64)
+    weight = np.asarray(weight, np.float32)
+    nt, nf, na, nd, npol = val.shape
+    basis = Basis(pp, r_0, beta)
+    coef = np.zeros_like(val)
+    resid = np.zeros_like(val)
+    w_out = weight.copy()
+    orders = np.zeros((nt, nf, na, npol), np.int32)
+    for p in range(npol):
+        for f in range(nf):
+            for a in range(na):
+                v = val[:, f, a, :, p].T
+                w = weight[:, f, a, :, p].T
+                if np.all(np.isnan(v)) or np.all(w == 0):
+                    continue
+                sc, rs, ww, oo = process_station_block(v, w, order, basis,
+                                                       "amplitude", niter,
+                                                       nsigma, adjust_order)
+                coef[:, f, a, :, p] = sc.T
+                resid[:, f, a, :, p] = rs.T
+                w_out[:, f, a, :, p] = ww.T
+                orders[:, f, a, p] = oo.astype(np.int32)
+    return dict(coef=coef, resid=resid, w_out=w_out, orders=orders)
+
+
+def interpolate_nearest(vals, src_times, src_freqs, dst_times, dst_freqs):
+    """screen.py:108-154 on log-amplitude coefficients: scipy interp1d
+    (kind="nearest", fill_value="extrapolate") along time then frequency."""
+    import scipy.interpolate as si
+    out = np.asarray(vals)
+    if len(src_times) == 1:
+        shape = list(out.shape)
+        shape[0] = len(dst_times)
+        shape[1] = len(dst_freqs)
+        return np.resize(out, shape)
+    if out.shape[0] != len(dst_times):
+        out = si.interp1d(src_times, out, axis=0, kind="nearest",
+                          fill_value="extrapolate")(dst_times)
+    if out.shape[1] != len(dst_freqs):
+        out = si.interp1d(src_freqs, out, axis=1, kind="nearest",
+                          fill_value="extrapolate")(dst_freqs)
+    return out

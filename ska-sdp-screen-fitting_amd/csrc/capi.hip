@@ -93,7 +93,7 @@ int sf_destroy(sf_ctx* ctx) {
   hipFree(ctx->d_pool_mask);
   hipFree(ctx->d_pool);
   hipFree(ctx->d_pos);
-  hipFree(ctx->d_slow);
+  hipFree(ctx->d_sigma);
   hipFree(ctx->d_class);
   hipFree(ctx->d_counters);
   hipFree(ctx->d_scratch);
@@ -216,12 +216,10 @@ int sf_kl_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,
              "sf_kl_fit: T, F, A must be >= 1");
   SF_REQUIRE((int64_t)F * A <= INT32_MAX / 2, SF_EINVAL,
              "sf_kl_fit: F * A too large");
-  SF_REQUIRE(p->screen_type == SF_SCREEN_PHASE || p->screen_type == SF_SCREEN_TEC,
+  SF_REQUIRE(p->screen_type == SF_SCREEN_PHASE || p->screen_type == SF_SCREEN_TEC ||
+                 p->screen_type == SF_SCREEN_AMPLITUDE,
              SF_EINVAL, "sf_kl_fit: unsupported screen type");
   SF_REQUIRE(p->niter >= 1, SF_EINVAL, "sf_kl_fit: niter must be >= 1");
-  SF_REQUIRE(p->screen_type == SF_SCREEN_PHASE || p->niter == 1, SF_EINVAL,
-             "sf_kl_fit: tec outlier iterations couple slots of a station "
-             "block and are not supported (use niter = 1)");
   SF_REQUIRE(p->ref_ant >= -1 && p->ant_offset >= 0, SF_EINVAL,
              "sf_kl_fit: bad ref_ant / ant_offset");
   {
@@ -300,7 +298,19 @@ int sf_kl_eval(sf_ctx* ctx, const double* coef, int64_t S, float* out,
              "sf_kl_eval: bad argument");
   if (S == 0) return SF_OK;
   SF_HIP(hipSetDevice(ctx->device));
-  return sf::launch_eval(ctx, coef, S, out, ring, flags);
+  return sf::launch_eval(ctx, coef, nullptr, nullptr, S, out, ring, flags);
+}
+
+int sf_kl_eval_gain(sf_ctx* ctx, const double* coef_phase,
+                    const double* coef_xx, const double* coef_yy, int64_t S,
+                    float* out, int64_t ring, unsigned flags) {
+  SF_REQUIRE(ctx && ctx->n_pix > 0 && ctx->d_cfrag, SF_EINVAL,
+             "sf_kl_eval_gain: call sf_set_grid first");
+  SF_REQUIRE(coef_phase && coef_xx && coef_yy && out && S >= 0 && ring >= 1,
+             SF_EINVAL, "sf_kl_eval_gain: bad argument");
+  if (S == 0) return SF_OK;
+  SF_HIP(hipSetDevice(ctx->device));
+  return sf::launch_eval(ctx, coef_phase, coef_xx, coef_yy, S, out, ring, flags);
 }
 
 int sf_tess_fill(sf_ctx* ctx, const int32_t* labels, int nx, int ny,

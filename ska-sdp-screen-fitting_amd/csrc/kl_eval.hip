@@ -101,10 +101,18 @@ __device__ __forceinline__ void store4(float* p, v4f v) {
   else *reinterpret_cast<v4f*>(p) = v;
 }
 
-template <int KS, bool VEC4, bool FAST, bool NT>
+template <bool FAST>
+__device__ __forceinline__ double amp10(double x) {
+  // amplitude screens are log10 values: 10 ** screen (kl_screen.py:338-365)
+  if (FAST) return (double)exp10f((float)x);
+  return exp10(x);
+}
+
+template <int KS, bool VEC4, bool FAST, bool NT, bool GAIN>
 __global__ __launch_bounds__(256, SF_EVAL_MIN_WAVES) void kl_eval_kernel(
-    const double* __restrict__ cfrag, const double* __restrict__ coef, int D,
-    int64_t S, int64_t P, int64_t n_pb, int64_t n_sc, int chunk_groups,
+    const double* __restrict__ cfrag, const double* __restrict__ coef,
+    const double* __restrict__ coef_xx, const double* __restrict__ coef_yy,
+    int D, int64_t S, int64_t P, int64_t n_pb, int64_t n_sc, int chunk_groups,
     float* __restrict__ out, int64_t ring, unsigned flags) {
   const int l = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
@@ -156,39 +164,69 @@ __global__ __launch_bounds__(256, SF_EVAL_MIN_WAVES) void kl_eval_kernel(
       for (int t = 0; t < kTiles; ++t)
         acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[kk], bf[kk][t],
                                                       acc[t], 0, 0, 0);
+    // gain: the XX / YY log-amplitude screens share the pixel basis
+    v4d accx[GAIN ? kTiles : 1], accy[GAIN ? kTiles : 1];
+    if (GAIN) {
+      const int64_t s = s0 + (l & 15);
+#pragma unroll
+      for (int t = 0; t < kTiles; ++t) {
+        accx[t] = v4d{0.0, 0.0, 0.0, 0.0};
+        accy[t] = v4d{0.0, 0.0, 0.0, 0.0};
+      }
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) {
+        const int d = 4 * kk + (l >> 4);
+        const bool ok = s < S && d < D;
+        const double ax = ok ? coef_xx[s * D + d] : 0.0;
+        const double ay = ok ? coef_yy[s * D + d] : 0.0;
+#pragma unroll
+        for (int t = 0; t < kTiles; ++t) {
+          accx[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ax, bf[kk][t], accx[t], 0, 0, 0);
+          accy[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ay, bf[kk][t], accy[t], 0, 0, 0);
+        }
+      }
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t s = s0 + acc_row(l, r);
       if (s >= S) continue;
-      float cv[kTiles], sv[kTiles];
+      // planes 0..3 = Re XX, Im XX, Re YY, Im YY
+      float pv[4][kTiles];
 #pragma unroll
       for (int t = 0; t < kTiles; ++t) {
-        jones_sincos<FAST>(acc[t][r], sv[t], cv[t]);
-        if (scrub) {
-          if (isnan(cv[t])) cv[t] = 1.0f;
-          if (isnan(sv[t])) sv[t] = 0.0f;
+        float sf, cf;
+        jones_sincos<FAST>(acc[t][r], sf, cf);
+        if (GAIN) {
+          // reference: A (fp64) * cos (fp64), one cast at the FITS store
+          const double ax = amp10<FAST>(accx[t][r]);
+          const double ay = amp10<FAST>(accy[t][r]);
+          pv[0][t] = (float)(ax * (double)cf);
+          pv[1][t] = (float)(ax * (double)sf);
+          pv[2][t] = (float)(ay * (double)cf);
+          pv[3][t] = (float)(ay * (double)sf);
+        } else {
+          pv[0][t] = pv[2][t] = cf;
+          pv[1][t] = pv[3][t] = sf;
         }
-        if (be) {
-          cv[t] = bswapf(cv[t]);
-          sv[t] = bswapf(sv[t]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (scrub && isnan(pv[q][t])) pv[q][t] = (q & 1) ? 0.0f : 1.0f;
+          if (be) pv[q][t] = bswapf(pv[q][t]);
         }
       }
       float* o = out + ((s % ring) * 4) * P + p0;
       if (VEC4) {
-        const v4f c4 = {cv[0], cv[1], cv[2], cv[3]};
-        const v4f s4 = {sv[0], sv[1], sv[2], sv[3]};
-        store4<NT>(o, c4);
-        store4<NT>(o + P, s4);
-        store4<NT>(o + 2 * P, c4);
-        store4<NT>(o + 3 * P, s4);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const v4f v = {pv[q][0], pv[q][1], pv[q][2], pv[q][3]};
+          store4<NT>(o + q * P, v);
+        }
       } else {
 #pragma unroll
         for (int t = 0; t < kTiles; ++t) {
           if (p0 + t < P) {
-            o[t] = cv[t];
-            o[P + t] = sv[t];
-            o[2 * P + t] = cv[t];
-            o[3 * P + t] = sv[t];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[q * P + t] = pv[q][t];
           }
         }
       }
@@ -208,7 +246,8 @@ int launch_cpix(sf_ctx* ctx, const double* d_x, const double* d_y) {
 }
 
 template <int KS>
-static int launch_eval_ks(sf_ctx* ctx, const double* coef, int64_t S,
+static int launch_eval_ks(sf_ctx* ctx, const double* coef,
+                          const double* cxx, const double* cyy, int64_t S,
                           float* out, int64_t ring, unsigned flags) {
   const int64_t P = ctx->n_pix;
   const int64_t n_pb = ctx->n_pix_blocks;
@@ -223,30 +262,40 @@ static int launch_eval_ks(sf_ctx* ctx, const double* coef, int64_t S,
   const bool vec4 = (P % 4 == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
   const bool fast = flags & SF_EVAL_FAST_SINCOS;
   const bool nt = flags & SF_EVAL_NT_STORES;
-#define SF_LAUNCH(V, F, N)                                                     \
-  hipLaunchKernelGGL((kl_eval_kernel<KS, V, F, N>), dim3((unsigned)nblk),      \
-                     dim3(256), 0, ctx->stream, ctx->d_cfrag, coef, ctx->D, S, \
-                     P, n_pb, n_sc, groups, out, ring, flags)
+  const bool gain = cxx != nullptr;
+#define SF_LAUNCH(V, F, N, G)                                                 \
+  hipLaunchKernelGGL((kl_eval_kernel<KS, V, F, N, G>), dim3((unsigned)nblk),  \
+                     dim3(256), 0, ctx->stream, ctx->d_cfrag, coef, cxx, cyy, \
+                     ctx->D, S, P, n_pb, n_sc, groups, out, ring, flags)
+#define SF_LAUNCH_G(V, F, N) \
+  do {                       \
+    if (gain)                \
+      SF_LAUNCH(V, F, N, true); \
+    else                     \
+      SF_LAUNCH(V, F, N, false); \
+  } while (0)
   if (vec4) {
     if (fast) {
-      if (nt) SF_LAUNCH(true, true, true); else SF_LAUNCH(true, true, false);
+      if (nt) SF_LAUNCH_G(true, true, true); else SF_LAUNCH_G(true, true, false);
     } else {
-      if (nt) SF_LAUNCH(true, false, true); else SF_LAUNCH(true, false, false);
+      if (nt) SF_LAUNCH_G(true, false, true); else SF_LAUNCH_G(true, false, false);
     }
   } else {
-    if (fast) SF_LAUNCH(false, true, false); else SF_LAUNCH(false, false, false);
+    if (fast) SF_LAUNCH_G(false, true, false); else SF_LAUNCH_G(false, false, false);
   }
+#undef SF_LAUNCH_G
 #undef SF_LAUNCH
   SF_HIP(hipGetLastError());
   return SF_OK;
 }
 
-int launch_eval(sf_ctx* ctx, const double* coef, int64_t S, float* out,
-                int64_t ring, unsigned flags) {
+int launch_eval(sf_ctx* ctx, const double* coef, const double* cxx,
+                const double* cyy, int64_t S, float* out, int64_t ring,
+                unsigned flags) {
   switch (ctx->ksteps) {
 #define SF_KS(k) \
   case k:        \
-    return launch_eval_ks<k>(ctx, coef, S, out, ring, flags);
+    return launch_eval_ks<k>(ctx, coef, cxx, cyy, S, out, ring, flags);
     SF_KS(1) SF_KS(2) SF_KS(3) SF_KS(4) SF_KS(5) SF_KS(6) SF_KS(7) SF_KS(8)
     SF_KS(9) SF_KS(10) SF_KS(11) SF_KS(12) SF_KS(13) SF_KS(14) SF_KS(15)
 #undef SF_KS

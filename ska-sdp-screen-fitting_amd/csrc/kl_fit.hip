@@ -572,6 +572,7 @@ int launch_basis(sf_ctx* ctx) {
 RefSpec ref_spec(const sf_fit_params* p, int A) {
   RefSpec r;
   const int ref = (p->ref_ant == -1) ? -1 : p->ref_ant - p->ant_offset;
+  if (p->screen_type == SF_SCREEN_AMPLITUDE) return r;  // never referenced
   if (p->screen_type == SF_SCREEN_PHASE) {
     if (p->ref_ant != -1) {
       if (p->ref_phase) r.refph = p->ref_phase; else r.sub = ref;

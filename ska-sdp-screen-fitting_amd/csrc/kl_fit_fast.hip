@@ -80,7 +80,7 @@ __global__ __launch_bounds__(256) void kl_classify_kernel(
     const int* __restrict__ st_order, const uint8_t* __restrict__ skip,
     int ref_skip, unsigned long long* __restrict__ keys, int cap,
     int* __restrict__ pos, uint8_t* __restrict__ cls,
-    int* __restrict__ slow_list, int* __restrict__ counters,
+    int* __restrict__ counters,
     double* __restrict__ coef, double* __restrict__ resid,
     float* __restrict__ w_out, int32_t* __restrict__ order_out) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -107,13 +107,8 @@ __global__ __launch_bounds__(256) void kl_classify_kernel(
     if (x > 0.0f) mask |= 1ull << d;
     tiny |= (x > 0.0f) && ((double)x <= kTinyW);
   }
-  if (tiny) {
-    cls[s] = 2;
-    pos[s] = -2;
-    slow_list[atomicAdd(counters + 2, 1)] = (int)s;
-    return;
-  }
-  cls[s] = 0;
+  if (tiny) atomicAdd(counters + 2, 1);
+  cls[s] = tiny ? 2 : 0;
   const unsigned long long full = (D == 64) ? ~0ull : ((1ull << D) - 1ull);
   if (mask == full) pos[s] = -1;
   else if (mask == 0ull) pos[s] = -2;
@@ -180,8 +175,10 @@ __global__ __launch_bounds__(64) void kl_subset_eig_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// 4. one fit pass (iteration `it` of _process_station) over all fast slots;
-//    one wavefront per slot.
+// 4. one fit pass (iteration `it` of _process_station) over the slots of one
+//    class; one wavefront per slot.  SLOW (class 2: a weight in (0, 1.001e-3])
+//    solves U_k^T W U_k by a Jacobi eigen-decomposition with the 1e-3 pinv
+//    cutoff; the fast class uses w I (uniform weights) or Cholesky.
 // ---------------------------------------------------------------------------
 struct FastLds {
   const double* U;    // [D][ld] full basis, columns sorted
@@ -190,14 +187,18 @@ struct FastLds {
   double* Vs;         // per wave: subset basis [D][ld]
   double* lams;       // per wave [64]
   double* G;          // per wave [D][ld]
+  double* M;          // per wave [D][ld] (SLOW: eigenvectors of G)
   double* vec;        // per wave [6][64]
+  double2* cs;        // per wave [64]   (SLOW: Jacobi scratch)
+  int2* pr;           // per wave [96]   (SLOW: Jacobi scratch)
 };
 
 __host__ __device__ inline size_t fast_shared_bytes(int D) {
   return (size_t)(2 * D * ldo(D) + 64) * sizeof(double);
 }
-__host__ __device__ inline size_t fast_wave_bytes(int D) {
-  return (size_t)(2 * D * ldo(D) + 64 + 6 * 64) * sizeof(double);
+__host__ __device__ inline size_t fast_wave_bytes(int D, bool slow) {
+  return (size_t)((slow ? 3 : 2) * D * ldo(D) + 64 + 6 * 64) * sizeof(double) +
+         (slow ? 64 * sizeof(double2) + 96 * sizeof(int2) : 0);
 }
 
 struct Basis {
@@ -207,9 +208,15 @@ struct Basis {
   const double* lam;
 };
 
+__device__ __forceinline__ double model_value(int screen_type, double x) {
+  // amplitude screens are log10 values (stationscreen.py:535-548, 576-588)
+  return screen_type == SF_SCREEN_AMPLITUDE ? pow(10.0, x) : x;
+}
+
 // One _fit_screen (stationscreen.py:433-594) in the eigenbasis.  Lanes p < n
 // carry the unflagged directions (phi_p, w_p); returns, per DIRECTION lane d,
 // white_d and resid_d.
+template <bool SLOW>
 __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
                          int K, int screen_type, bool uniform, double wu,
                          double phi_p, double w_p, double phi_d, double w_d,
@@ -220,6 +227,7 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
   double* v0 = L.vec;
   double* v1 = L.vec + 64;
   double* v2 = L.vec + 128;
+  double* v3 = L.vec + 192;
   double rc = 0.0, rs = 0.0;
   if (l < n) {
     if (screen_type == SF_SCREEN_PHASE) {
@@ -227,6 +235,8 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
       sincos(phi_p, &sn, &cn);
       rc = w_p * cn;
       rs = w_p * sn;
+    } else if (screen_type == SF_SCREEN_AMPLITUDE) {
+      rc = w_p * log10(phi_p);
     } else {
       rc = w_p * phi_p;
     }
@@ -244,7 +254,7 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
     }
   }
   if (K > 0) {
-    if (uniform) {
+    if (!SLOW && uniform) {
       // U_k^T (w I) U_k = w I  (U_k orthonormal over the unflagged rows)
       a1 /= wu;
       a2 /= wu;
@@ -258,7 +268,43 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
         }
       }
       lds_sync();
-      wave_cholesky_solve2(L.G, K, ld, a1, a2);
+      if (!SLOW) {
+        wave_cholesky_solve2(L.G, K, ld, a1, a2);
+      } else {
+        // pinv(G, atol=1e-3) = sum_{|mu| > 1e-3} z z^T / mu (scipy >= 1.7)
+        wave_jacobi(L.G, L.M, L.cs, L.pr, K, ld, 40);
+        if (l < K) {
+          v0[l] = a1;
+          v1[l] = a2;
+        }
+        lds_sync();
+        double t1 = 0.0, t2 = 0.0;
+        if (l < K) {
+          for (int q = 0; q < K; ++q) {
+            t1 += L.M[q * ld + l] * v0[q];
+            t2 += L.M[q * ld + l] * v1[q];
+          }
+          const double mu = L.G[l * ld + l];
+          if (fabs(mu) > kAtol) {
+            t1 /= mu;
+            t2 /= mu;
+          } else {
+            t1 = t2 = 0.0;
+          }
+        }
+        lds_sync();
+        if (l < K) {
+          v2[l] = t1;
+          v3[l] = t2;
+        }
+        lds_sync();
+        a1 = a2 = 0.0;
+        if (l < K)
+          for (int m = 0; m < K; ++m) {
+            a1 += L.M[l * ld + m] * v2[m];
+            a2 += L.M[l * ld + m] * v3[m];
+          }
+      }
     }
   }
   lds_sync();
@@ -277,11 +323,7 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
       cre += u * v0[k];
       cim += u * v1[k];
     }
-    if (screen_type == SF_SCREEN_PHASE) {
-      screen = atan2(cim, cre);
-    } else {
-      screen = cre;
-    }
+    screen = (screen_type == SF_SCREEN_PHASE) ? atan2(cim, cre) : cre;
   }
   lds_sync();
   if (l < n) v2[l] = screen;
@@ -307,7 +349,7 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
   lds_sync();
   if (B.full) {
     white_d = white;
-    resid_d = phi_d - cw;
+    resid_d = phi_d - model_value(screen_type, cw);
     return;
   }
   // flagged directions (stationscreen.py:565-582): screen from the subset's
@@ -352,22 +394,28 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
     for (int r = 0; r < D; ++r) wa += L.U[l * ld + r] * v0[r];
   lds_sync();
   white_d = wa;
-  resid_d = phi_d - sall;
+  resid_d = phi_d - model_value(screen_type, sall);
 }
 
-#ifndef SF_FIT_MIN_WAVES
-#define SF_FIT_MIN_WAVES 1
-#endif
-__global__ __launch_bounds__(256, SF_FIT_MIN_WAVES) void kl_fit_pass_kernel(
+// residual as the outlier test / chi^2 see it (stationscreen.py:660-668,
+// 733-746): phase & tec use the residual, amplitude the log10 ratio
+__device__ __forceinline__ double screen_diff(int screen_type, double val,
+                                              double resid) {
+  if (screen_type == SF_SCREEN_AMPLITUDE)
+    return log10(val) - log10(fabs(val - resid));
+  return resid;
+}
+
+template <bool SLOW>
+__global__ __launch_bounds__(256) void kl_fit_pass_kernel(
     int it, int niter, int64_t S, int F, int A, int D,
     const double* __restrict__ phase, const double* __restrict__ refph,
     int ref_sub, const double* __restrict__ g_u, const double* __restrict__ g_c,
     const double* __restrict__ g_eig, const int* __restrict__ st_order,
-    uint8_t* __restrict__ cls, int* __restrict__ pos,
+    const uint8_t* __restrict__ cls, int* __restrict__ pos,
     const int* __restrict__ ids, unsigned long long* __restrict__ keys, int cap,
-    const double* __restrict__ pool, int pool_cap,
-    int* __restrict__ slow_list, int* __restrict__ counters, int screen_type,
-    double nsigma, int adjust_order, double* __restrict__ coef,
+    const double* __restrict__ pool, int pool_cap, int* __restrict__ counters,
+    int screen_type, double nsigma, int adjust_order, double* __restrict__ coef,
     double* __restrict__ resid, float* __restrict__ w_out,
     int32_t* __restrict__ order_out) {
 #pragma clang fp contract(off)
@@ -390,33 +438,30 @@ __global__ __launch_bounds__(256, SF_FIT_MIN_WAVES) void kl_fit_pass_kernel(
   L.U = sU;
   L.C = sC;
   L.lam = sl;
-  double* wb = sl + 64 + (size_t)wv * (fast_wave_bytes(D) / sizeof(double));
+  double* wb = sl + 64 + (size_t)wv * (fast_wave_bytes(D, SLOW) / sizeof(double));
   L.Vs = wb;
   L.G = wb + D * ld;
-  L.lams = L.G + D * ld;
+  L.M = L.G + D * ld;
+  L.lams = (SLOW ? L.M + D * ld : L.G + D * ld);
   L.vec = L.lams + 64;
+  L.cs = reinterpret_cast<double2*>(L.vec + 6 * 64);
+  L.pr = reinterpret_cast<int2*>(L.cs + 64);
+  const uint8_t want = SLOW ? 2 : 0;
 
   for (int64_t s = (int64_t)blockIdx.x * nwaves + wv; s < S;
        s += (int64_t)gridDim.x * nwaves) {
-    if (cls[s] != 0) continue;
+    if (cls[s] != want) continue;
     const int a = (int)(s % A);
-    int p0 = pos[s];
-    // basis of the current mask
+    const int p0 = pos[s];
     int id = -1;
     if (p0 >= 0) {
       id = ids[p0];
-      if (id < 0 || id >= pool_cap) {  // pool overflow: general kernel
-        if (d == 0) {
-          cls[s] = 2;
-          slow_list[atomicAdd(counters + 2, 1)] = (int)s;
-        }
+      if (id < 0 || id >= pool_cap) {  // cannot happen: flag it loudly
+        if (d == 0) atomicOr(counters + 3, 1);
         continue;
       }
-    } else if (p0 == -3) {  // hash table full: general kernel
-      if (d == 0) {
-        cls[s] = 2;
-        slow_list[atomicAdd(counters + 2, 1)] = (int)s;
-      }
+    } else if (p0 == -3) {
+      if (d == 0) atomicOr(counters + 3, 2);
       continue;
     }
     const int64_t base = s * D;
@@ -473,8 +518,8 @@ __global__ __launch_bounds__(256, SF_FIT_MIN_WAVES) void kl_fit_pass_kernel(
     if (n_unfl > 0) {
       if (order > n_unfl - 1) order = n_unfl - 1;
       if (it == 0) {
-        fit_once(L, B, D, ld, (int)order, screen_type, uniform, wmin, phi_p,
-                 w_p, phi_d, w_d, white_d, resid_d);
+        fit_once<SLOW>(L, B, D, ld, (int)order, screen_type, uniform, wmin,
+                       phi_p, w_p, phi_d, w_d, white_d, resid_d);
       } else if (adjust_order) {
         bool hit_upper = false, hit_lower = false, hit_upper2 = false,
              hit_lower2 = false;
@@ -482,8 +527,8 @@ __global__ __launch_bounds__(256, SF_FIT_MIN_WAVES) void kl_fit_pass_kernel(
         for (int oi = 0; oi < 4; ++oi) {
           // oi == 0: the weights always compare equal (quirk Q2) -> no fit
           if (oi > 0)
-            fit_once(L, B, D, ld, (int)order, screen_type, uniform, wmin,
-                     phi_p, w_p, phi_d, w_d, white_d, resid_d);
+            fit_once<SLOW>(L, B, D, ld, (int)order, screen_type, uniform, wmin,
+                           phi_p, w_p, phi_d, w_d, white_d, resid_d);
           if (hit_lower2 || hit_upper2) break;
           double redchi2;
           if (screen_type == SF_SCREEN_PHASE) {
@@ -495,8 +540,13 @@ __global__ __launch_bounds__(256, SF_FIT_MIN_WAVES) void kl_fit_pass_kernel(
             const double m2 = wave_sum(cn * cn * ww) / sw;
             redchi2 = (1.0 - hypot(m1, m2)) * sw / (n_unfl - order);
           } else {
-            const double ww = unfl ? w_d : 0.0;
-            redchi2 = wave_sum(resid_d * resid_d * ww) / (n_unfl - order);
+            // np.sum(square(diff) * w) over all directions
+            double t = 0.0;
+            if (d < D) {
+              const double sd = screen_diff(screen_type, phi_d, resid_d);
+              t = (sd * sd) * w_d;
+            }
+            redchi2 = wave_sum(t) / (n_unfl - order);
           }
           if (oi > 0) {
             if (redchi2 > 1.0 && prev_redchi2 < redchi2) sign = -sign;
@@ -521,7 +571,9 @@ __global__ __launch_bounds__(256, SF_FIT_MIN_WAVES) void kl_fit_pass_kernel(
         }
       }
     }
-    // outlier flagging for the next pass (stationscreen.py:303-350, 660-671)
+    // phase: outlier flagging for the next pass, per slot (the circular
+    // sigma is per time across directions, stationscreen.py:303-350);
+    // tec / amplitude: one sigma per station block -> kl_block_sigma/flag
     if (it + 1 < niter && screen_type == SF_SCREEN_PHASE) {
       const bool live = d < D;
       if (__any(live && w_d > 0.0)) {
@@ -549,6 +601,77 @@ __global__ __launch_bounds__(256, SF_FIT_MIN_WAVES) void kl_fit_pass_kernel(
       w_out[base + d] = (float)w_d;
     }
     if (d == 0) order_out[s] = (int32_t)order;
+  }
+}
+
+// 5. tec / amplitude outlier sigma per (station, freq) block
+//    (stationscreen.py:338-344: fancy indexing flattens the block, so ONE
+//    weighted rms over all its times and directions, quirk Q6)
+__global__ __launch_bounds__(256) void kl_block_sigma_kernel(
+    int T, int F, int A, int D, const double* __restrict__ phase,
+    const double* __restrict__ refph, int ref_sub,
+    const uint8_t* __restrict__ skip, int ref_skip, int screen_type,
+    const double* __restrict__ resid, const float* __restrict__ w_out,
+    double* __restrict__ sigma) {
+  __shared__ double red[2][256];
+  const int blk = blockIdx.x;  // f * A + a
+  const int f = blk / A, a = blk % A;
+  double sw = 0.0, swr = 0.0;
+  if (!(skip[blk] || a == ref_skip)) {
+    for (int e = threadIdx.x; e < T * D; e += blockDim.x) {
+      const int t = e / D, d = e % D;
+      const int64_t s = ((int64_t)t * F + f) * A + a;
+      const double w = (double)w_out[s * D + d];
+      if (w > 0.0) {
+        const double v = phase_ref(phase, refph, ref_sub, s, a, A, D, d);
+        const double sd = screen_diff(screen_type, v, resid[s * D + d]);
+        swr += w * (sd * sd);
+        sw += w;
+      }
+    }
+  }
+  red[0][threadIdx.x] = sw;
+  red[1][threadIdx.x] = swr;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + o];
+      red[1][threadIdx.x] += red[1][threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) sigma[blk] = sqrt(red[1][0] / red[0][0]);
+}
+
+// 6. apply the block sigma: |diff| > nsigma sigma -> weight 0, new mask
+__global__ __launch_bounds__(256) void kl_block_flag_kernel(
+    int64_t S, int F, int A, int D, const double* __restrict__ phase,
+    const double* __restrict__ refph, int ref_sub,
+    const uint8_t* __restrict__ cls, int screen_type, double nsigma,
+    const double* __restrict__ sigma, const double* __restrict__ resid,
+    float* __restrict__ w_out, unsigned long long* __restrict__ keys, int cap,
+    int* __restrict__ pos) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S || (cls[s] != 0 && cls[s] != 2)) return;
+  const int a = (int)(s % A);
+  const int f = (int)((s / A) % F);
+  const double sig = sigma[f * A + a];
+  unsigned long long m = 0ull;
+  bool changed = false;
+  for (int d = 0; d < D; ++d) {
+    float w = w_out[s * D + d];
+    const double v = phase_ref(phase, refph, ref_sub, s, a, A, D, d);
+    const double sd = screen_diff(screen_type, v, resid[s * D + d]);
+    if (fabs(sd) > nsigma * sig && w != 0.0f) {
+      w = 0.0f;
+      w_out[s * D + d] = w;
+      changed = true;
+    }
+    if (w > 0.0f) m |= 1ull << d;
+  }
+  if (changed) {
+    const unsigned long long full = (D == 64) ? ~0ull : ((1ull << D) - 1ull);
+    pos[s] = (m == 0ull) ? -2 : (m == full ? -1 : table_insert(keys, cap, m));
   }
 }
 
@@ -617,7 +740,7 @@ __global__ __launch_bounds__(256) void kl_fill_mask_kernel(
 }
 
 // number new masks, make sure the pool holds them, decompose them
-static int number_and_decompose(sf_ctx* ctx) {
+static int number_and_decompose(sf_ctx* ctx, int* n_slow) {
   SF_HIP(hipMemcpyAsync(ctx->d_counters + 1, ctx->d_counters, sizeof(int),
                         hipMemcpyDeviceToDevice, ctx->stream));
   const int cap = (int)ctx->table_cap;
@@ -626,10 +749,11 @@ static int number_and_decompose(sf_ctx* ctx) {
                      ctx->stream, ctx->d_keys, cap, ctx->d_ids,
                      ctx->d_pool_mask, old_cap, ctx->d_counters);
   SF_HIP(hipGetLastError());
-  int cnt[2];
-  SF_HIP(hipMemcpyAsync(cnt, ctx->d_counters, 2 * sizeof(int),
+  int cnt[3];
+  SF_HIP(hipMemcpyAsync(cnt, ctx->d_counters, 3 * sizeof(int),
                         hipMemcpyDeviceToHost, ctx->stream));
   SF_HIP(hipStreamSynchronize(ctx->stream));
+  *n_slow = cnt[2];
   if (cnt[0] > old_cap) {
     SF_TRYF(ensure_pool(ctx, (size_t)cnt[0]));
     hipLaunchKernelGGL(kl_fill_mask_kernel, dim3((cap + 255) / 256), dim3(256),
@@ -656,6 +780,34 @@ static int number_and_decompose(sf_ctx* ctx) {
   return SF_OK;
 }
 
+template <bool SLOW>
+static int launch_pass(sf_ctx* ctx, int it, const sf_fit_params* p,
+                       const RefSpec& r, int64_t S, int F, int A,
+                       const double* phase, double* coef, double* resid,
+                       float* w_out, int32_t* order_out) {
+  const int D = ctx->D;
+  const size_t shared = fast_shared_bytes(D);
+  const size_t wave = fast_wave_bytes(D, SLOW);
+  int nw = 4;
+  while (nw > 1 && shared + nw * wave > 64 * 1024) --nw;
+  const size_t shm = shared + nw * wave;
+  if (shm > 64 * 1024)
+    SF_HIP(hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&kl_fit_pass_kernel<SLOW>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+  int64_t blocks = (S + nw - 1) / nw;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL((kl_fit_pass_kernel<SLOW>), dim3((unsigned)blocks),
+                     dim3(64 * nw), shm, ctx->stream, it, p->niter, S, F, A, D,
+                     phase, r.refph, r.sub, ctx->d_u, ctx->d_c, ctx->d_eig,
+                     ctx->d_st_order, ctx->d_class, ctx->d_pos, ctx->d_ids,
+                     ctx->d_keys, (int)ctx->table_cap, ctx->d_pool,
+                     (int)ctx->pool_cap, ctx->d_counters, p->screen_type,
+                     p->nsigma, p->adjust_order, coef, resid, w_out, order_out);
+  SF_HIP(hipGetLastError());
+  return SF_OK;
+}
+
 int launch_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,
                int F, int A, const sf_fit_params* p, double* coef,
                double* resid, float* w_out, int32_t* order_out) {
@@ -666,6 +818,10 @@ int launch_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,
 
   static const char* env = std::getenv("SCREENFIT_FIT");
   if (ctx->force_general || (env && env[0] == 'g')) {
+    if (p->screen_type == SF_SCREEN_AMPLITUDE || p->niter > 1 && p->screen_type != SF_SCREEN_PHASE) {
+      set_error("the general fit kernel handles phase (any niter) and tec (niter 1) only");
+      return SF_EINVAL;
+    }
     return launch_fit_general(ctx, nullptr, nullptr, S, phase, weight, T, F, A,
                               p, r, coef, resid, w_out, order_out);
   }
@@ -686,18 +842,24 @@ int launch_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,
     if (!order_out) order_out = ctx->d_oscratch;
   }
   if (ctx->slot_cap < (size_t)S) {
-    size_t c1 = 0, c2 = 0, c3 = 0;
+    size_t c1 = 0, c3 = 0;
     if (ctx->d_pos) (void)hipFree(ctx->d_pos);
-    if (ctx->d_slow) (void)hipFree(ctx->d_slow);
     if (ctx->d_class) (void)hipFree(ctx->d_class);
-    ctx->d_pos = ctx->d_slow = nullptr;
+    ctx->d_pos = nullptr;
     ctx->d_class = nullptr;
     SF_TRYF(grow(&ctx->d_pos, c1, (size_t)S));
-    SF_TRYF(grow(&ctx->d_slow, c2, (size_t)S));
     SF_TRYF(grow(&ctx->d_class, c3, (size_t)S));
     ctx->slot_cap = (size_t)S;
   }
-  const size_t tcap = next_pow2((size_t)(2 * p->niter) * (size_t)S + 64);
+  if (ctx->sigma_cap < (size_t)F * A) {
+    size_t c = 0;
+    if (ctx->d_sigma) (void)hipFree(ctx->d_sigma);
+    ctx->d_sigma = nullptr;
+    SF_TRYF(grow(&ctx->d_sigma, c, (size_t)F * A));
+    ctx->sigma_cap = (size_t)F * A;
+  }
+  // every pass inserts at most one mask per slot
+  const size_t tcap = next_pow2((size_t)(2 * p->niter + 2) * (size_t)S + 64);
   if (ctx->table_cap < tcap) {
     size_t c1 = 0, c2 = 0;
     if (ctx->d_keys) (void)hipFree(ctx->d_keys);
@@ -722,37 +884,39 @@ int launch_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,
   hipLaunchKernelGGL(kl_classify_kernel, dim3((unsigned)((S + 255) / 256)),
                      dim3(256), 0, ctx->stream, weight, S, F, A, D,
                      ctx->d_st_order, ctx->d_skip, r.skip, ctx->d_keys, cap,
-                     ctx->d_pos, ctx->d_class, ctx->d_slow, ctx->d_counters,
-                     coef, resid, w_out, order_out);
+                     ctx->d_pos, ctx->d_class, ctx->d_counters, coef, resid,
+                     w_out, order_out);
   SF_HIP(hipGetLastError());
 
-  const size_t shared = fast_shared_bytes(D);
-  const size_t wave = fast_wave_bytes(D);
-  int nw = 4;
-  while (nw > 1 && shared + nw * wave > 64 * 1024) --nw;
-  const size_t shm = shared + nw * wave;
-  if (shm > 64 * 1024)
-    SF_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&kl_fit_pass_kernel),
-                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)shm));
-  int64_t blocks = (S + nw - 1) / nw;
-  if (blocks > 16384) blocks = 16384;
+  const bool block_flags = p->screen_type != SF_SCREEN_PHASE;
   for (int it = 0; it < p->niter; ++it) {
-    SF_TRYF(number_and_decompose(ctx));
-    hipLaunchKernelGGL(kl_fit_pass_kernel, dim3((unsigned)blocks),
-                       dim3(64 * nw), shm, ctx->stream, it, p->niter, S, F, A,
-                       D, phase, r.refph, r.sub, ctx->d_u, ctx->d_c,
-                       ctx->d_eig, ctx->d_st_order, ctx->d_class, ctx->d_pos,
-                       ctx->d_ids, ctx->d_keys, cap, ctx->d_pool,
-                       (int)ctx->pool_cap, ctx->d_slow, ctx->d_counters,
-                       p->screen_type, p->nsigma, p->adjust_order, coef, resid,
-                       w_out, order_out);
-    SF_HIP(hipGetLastError());
+    int n_slow = 0;
+    SF_TRYF(number_and_decompose(ctx, &n_slow));
+    SF_TRYF(launch_pass<false>(ctx, it, p, r, S, F, A, phase, coef, resid,
+                               w_out, order_out));
+    if (n_slow > 0)
+      SF_TRYF(launch_pass<true>(ctx, it, p, r, S, F, A, phase, coef, resid,
+                                w_out, order_out));
+    if (block_flags && it + 1 < p->niter) {
+      hipLaunchKernelGGL(kl_block_sigma_kernel, dim3(F * A), dim3(256), 0,
+                         ctx->stream, T, F, A, D, phase, r.refph, r.sub,
+                         ctx->d_skip, r.skip, p->screen_type, resid, w_out,
+                         ctx->d_sigma);
+      SF_HIP(hipGetLastError());
+      hipLaunchKernelGGL(kl_block_flag_kernel, dim3((unsigned)((S + 255) / 256)),
+                         dim3(256), 0, ctx->stream, S, F, A, D, phase, r.refph,
+                         r.sub, ctx->d_class, p->screen_type, p->nsigma,
+                         ctx->d_sigma, resid, w_out, ctx->d_keys, cap,
+                         ctx->d_pos);
+      SF_HIP(hipGetLastError());
+    }
   }
-  // slow path: tiny weights / overflow, recomputed from scratch
-  return launch_fit_general(ctx, ctx->d_slow, ctx->d_counters + 2, S, phase,
-                            weight, T, F, A, p, r, coef, resid, w_out,
-                            order_out);
+  int err = 0;
+  SF_HIP(hipMemcpyAsync(&err, ctx->d_counters + 3, sizeof(int),
+                        hipMemcpyDeviceToHost, ctx->stream));
+  SF_HIP(hipStreamSynchronize(ctx->stream));
+  SF_REQUIRE(err == 0, SF_EIO, "sf_kl_fit: internal mask table overflow");
+  return SF_OK;
 }
 
 }  // namespace sf

@@ -70,10 +70,11 @@ struct sf_ctx {
   size_t pool_cap = 0;
   int pool_D = 0;
   int* d_pos = nullptr;                  // [S] table slot of the current mask
-  int* d_slow = nullptr;                 // [S] slow-path slot list
   uint8_t* d_class = nullptr;            // [S] 0 fast, 1 skipped, 2 slow
+  double* d_sigma = nullptr;             // [F][A] tec/amplitude block sigma
+  size_t sigma_cap = 0;
   size_t slot_cap = 0;
-  int* d_counters = nullptr;             // [0] ids, [1] range start, [2] slow
+  int* d_counters = nullptr;  // [0] ids, [1] range start, [2] slow, [3] error
   double* d_scratch = nullptr;           // resid / state when caller passes NULL
   size_t scratch_cap = 0;
   float* d_wscratch = nullptr;
@@ -103,8 +104,9 @@ int launch_cpix(sf_ctx* ctx, const double* d_x, const double* d_y);
 int launch_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,
                int F, int A, const sf_fit_params* p, double* coef,
                double* resid, float* w_out, int32_t* order_out);
-int launch_eval(sf_ctx* ctx, const double* coef, int64_t S, float* out,
-                int64_t ring, unsigned flags);
+int launch_eval(sf_ctx* ctx, const double* coef, const double* cxx,
+                const double* cyy, int64_t S, float* out, int64_t ring,
+                unsigned flags);
 int launch_tess(sf_ctx* ctx, const int32_t* labels, int nx, int ny,
                 const double* phase, const double* amp_xx,
                 const double* amp_yy, int D, int64_t S, float* out,

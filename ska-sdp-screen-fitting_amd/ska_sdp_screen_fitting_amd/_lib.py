@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("SCREENFIT_LIB", os.path.join(_HERE, "libscreenfit.so"
 
 SF_SCREEN_PHASE = 0
 SF_SCREEN_TEC = 1
+SF_SCREEN_AMPLITUDE = 2
 SF_EVAL_NAN_SCRUB = 1
 SF_EVAL_FAST_SINCOS = 1 << 8
 SF_EVAL_NT_STORES = 1 << 9
@@ -27,7 +28,7 @@ EXPORTED = (
     "sf_version", "sf_last_error", "sf_create", "sf_destroy", "sf_set_stream",
     "sf_synchronize", "sf_set_option", "sf_alloc", "sf_free", "sf_copy_h2d", "sf_copy_d2h",
     "sf_set_basis", "sf_get_basis", "sf_kl_fit", "sf_get_fit_stats",
-    "sf_set_grid", "sf_kl_eval", "sf_tess_fill",
+    "sf_set_grid", "sf_kl_eval", "sf_kl_eval_gain", "sf_tess_fill",
 )
 
 
@@ -81,6 +82,8 @@ def load_library(path=None):
             "sf_get_fit_stats": ([vp, ip, ip], c_int),
             "sf_set_grid": ([vp, vp, c_int, vp, c_int], c_int),
             "sf_kl_eval": ([vp, vp, i64, vp, i64, ctypes.c_uint], c_int),
+            "sf_kl_eval_gain": ([vp, vp, vp, vp, i64, vp, i64, ctypes.c_uint],
+                                c_int),
             "sf_tess_fill": ([vp, vp, c_int, c_int, vp, vp, vp, c_int, i64, vp,
                               i64, c_dbl, ctypes.c_uint], c_int),
         }
@@ -199,6 +202,14 @@ class Context:
         _check(self.lib.sf_kl_eval(self.h, _ptr(coef), int(S), _ptr(out),
                                    max(ring, 1), int(flags)), "sf_kl_eval")
 
+
+    def eval_gain(self, coef_ph, coef_xx, coef_yy, S, out, ring_slots=None,
+                  flags=SF_EVAL_NAN_SCRUB | SF_EVAL_FAST_SINCOS | SF_EVAL_NT_STORES):
+        ring = int(S if ring_slots is None else ring_slots)
+        _check(self.lib.sf_kl_eval_gain(self.h, _ptr(coef_ph), _ptr(coef_xx),
+                                        _ptr(coef_yy), int(S), _ptr(out),
+                                        max(ring, 1), int(flags)),
+               "sf_kl_eval_gain")
 
     def tess_fill(self, labels, nx, ny, phase, D, S, out, ring_slots=None,
                   amp_xx=None, amp_yy=None, smooth_pix=0.0,

@@ -65,12 +65,35 @@ class KLEvaluator:
             self.ctx.eval(coef_dev, S, out_dev, S, flags)
         return out_dev
 
-    def eval_host(self, coef, flags=DEFAULT_FLAGS):
-        """coef: host [..., D] -> host float32 [..., 4, ny, nx]."""
-        coef = np.ascontiguousarray(coef, np.float64)
+    def eval_gain_device(self, coef_dev, xx_dev, yy_dev, out_dev=None,
+                         flags=DEFAULT_FLAGS):
+        """Phase + XX / YY log10-amplitude coefficients (device [S, D] each)
+        -> device [S, 4, ny, nx] gain planes."""
+        torch = self.torch
+        S = coef_dev.shape[0]
+        if out_dev is None:
+            out_dev = torch.empty((S, 4, self.ny, self.nx), dtype=torch.float32,
+                                  device=self.dev)
+        with torch.cuda.device(self.dev):
+            self.ctx.set_stream(torch.cuda.current_stream(self.dev).cuda_stream)
+            self.ctx.eval_gain(coef_dev, xx_dev, yy_dev, S, out_dev, S, flags)
+        return out_dev
+
+    def _upload(self, a):
+        a = np.ascontiguousarray(a, np.float64)
+        return self.torch.from_numpy(a.reshape(-1, self.D)).to(self.dev)
+
+    def eval_host(self, coef, amp_xx=None, amp_yy=None, flags=DEFAULT_FLAGS):
+        """coef (and optional log10-amplitude coefs): host [..., D] -> host
+        float32 [..., 4, ny, nx]."""
+        coef = np.asarray(coef)
         lead = coef.shape[:-1]
-        c = self.torch.from_numpy(coef.reshape(-1, self.D)).to(self.dev)
-        out = self.eval_device(c, flags=flags)
+        c = self._upload(coef)
+        if amp_xx is None:
+            out = self.eval_device(c, flags=flags)
+        else:
+            out = self.eval_gain_device(c, self._upload(amp_xx),
+                                        self._upload(amp_yy), flags=flags)
         return out.cpu().numpy().reshape(lead + (4, self.ny, self.nx))
 
 
@@ -93,10 +116,10 @@ class KLScreen(Screen):
         self._evaluators = {}
 
     def fit(self):
-        """Fit screens to the input solutions (kl_screen.py:61-155)."""
-        if not self.phase_only:
-            raise NotImplementedError(
-                "amplitude (gain) KL screens are the next row of the build")
+        """Fit screens to the input solutions (kl_screen.py:61-155): phases
+        with per-station orders referenced to a central station; for gain
+        solutions also the XX / YY log10 amplitudes (order
+        min(12, max(3, round(D / 2))), 3 iterations, no order scaling)."""
         h5 = H5parm(self.input_h5parm_filename)
         solset = h5.get_solset(self.input_solset_name)
         soltab_ph = solset.get_soltab(self.input_phase_soltab_name)
@@ -111,6 +134,17 @@ class KLScreen(Screen):
         stationscreen.run(soltab_ph, "phase_screen000", order=screen_order,
                           ref_ant=ref_ind, scale_order=True, adjust_order=True,
                           ncpu=self.ncpu or 0, device=self.device)
+        if not self.phase_only:
+            soltab_amp = solset.get_soltab(self.input_amplitude_soltab_name)
+            order_amp = min(12, max(3, int(np.round(len(dirs) / 2))))
+            stationscreen.run(soltab_amp, "amplitude_screen000", order=order_amp,
+                              niter=3, scale_order=False, adjust_order=True,
+                              ncpu=self.ncpu or 0, device=self.device)
+            sta = solset.get_soltab("amplitude_screen000")
+            self.log_amps = True
+            self.vals_amp = sta.val
+            self.times_amp = np.asarray(sta.time)
+            self.freqs_amp = np.asarray(sta.freq)
         st = solset.get_soltab("phase_screen000")
         self.vals_ph = st.val
         self.times_ph = np.asarray(st.time)
@@ -154,9 +188,13 @@ class KLScreen(Screen):
         """(t_stop - t_start, 4, ny, nx) float64 (kl_screen.py:192-380); the
         values carry the float32 rounding of the FITS cube (Q12)."""
         del out_dir, ncpu
-        coef = np.asarray(self.vals_ph)[t_start_index:t_stop_index, freq_ind,
-                                        stat_ind, :]
-        return self.evaluator(cellsize_deg).eval_host(coef).astype(np.float64)
+        sl = np.s_[t_start_index:t_stop_index, freq_ind, stat_ind, :]
+        coef = np.asarray(self.vals_ph)[sl]
+        ev = self.evaluator(cellsize_deg)
+        if self.phase_only:
+            return ev.eval_host(coef).astype(np.float64)
+        amp = np.asarray(self.vals_amp)[sl]
+        return ev.eval_host(coef, amp[..., 0], amp[..., 1]).astype(np.float64)
 
     def write_chunk(self, writer, g_start, g_stop, cellsize_deg, smooth_pix,
                     max_batch_bytes=1 << 30):
@@ -172,8 +210,10 @@ class KLScreen(Screen):
         row_bytes = n_f * n_a * per_slot
         rows = max(1, int(max_batch_bytes // row_bytes))
         rows = min(rows, g_stop - g_start)
-        coef = torch.from_numpy(np.ascontiguousarray(
-            vals[g_start:g_stop].reshape(-1, D), np.float64)).to(ev.dev)
+        coef = ev._upload(vals[g_start:g_stop])
+        if not self.phase_only:
+            amp = np.asarray(self.vals_amp)[g_start:g_stop]
+            c_xx, c_yy = ev._upload(amp[..., 0]), ev._upload(amp[..., 1])
         pipe = PinnedPipeline(torch, ev.dev, rows * row_bytes)
         try:
             for t0 in range(g_start, g_stop, rows):
@@ -181,7 +221,12 @@ class KLScreen(Screen):
                 s0, s1 = (t0 - g_start) * n_f * n_a, (t1 - g_start) * n_f * n_a
                 slot, buf = pipe.device_buffer((s1 - s0) * per_slot)
                 out = buf.view(torch.float32).view(s1 - s0, 4, ev.ny, ev.nx)
-                ev.eval_device(coef[s0:s1], out, DEFAULT_FLAGS | SF_EVAL_BIG_ENDIAN)
+                flags = DEFAULT_FLAGS | SF_EVAL_BIG_ENDIAN
+                if self.phase_only:
+                    ev.eval_device(coef[s0:s1], out, flags)
+                else:
+                    ev.eval_gain_device(coef[s0:s1], c_xx[s0:s1], c_yy[s0:s1],
+                                        out, flags)
                 pipe.submit(slot, (s1 - s0) * per_slot, writer)
         finally:
             pipe.close()

@@ -73,6 +73,27 @@ def time_chunks(times, mem_per_slot_gb, available_gb=None):
     return [int(g) for g in gaps_ind]
 
 
+def nearest_index(src, dst):
+    """Index of the nearest ``src`` sample for every ``dst`` point, ties to
+    the lower sample, clamped at the ends (scipy interp1d kind="nearest"
+    with fill_value="extrapolate")."""
+    src = np.asarray(src, np.float64)
+    order = np.argsort(src, kind="mergesort")
+    xs = src[order]
+    bounds = (xs[1:] + xs[:-1]) / 2.0
+    idx = np.searchsorted(bounds, np.asarray(dst, np.float64), side="left")
+    return order[np.clip(idx, 0, len(xs) - 1)]
+
+
+def resample_axis(src, vals, dst, axis, kind="nearest"):
+    """One axis of Screen.interpolate; "nearest" is an exact row gather."""
+    if kind == "nearest":
+        return np.take(vals, nearest_index(src, dst), axis=axis)
+    import scipy.interpolate as si
+    return si.interp1d(src, vals, axis=axis, kind=kind,
+                       fill_value="extrapolate")(dst)
+
+
 class Screen:
     """Master class for a-term screens (screen.py:19)."""
 
@@ -112,10 +133,27 @@ class Screen:
         """Implemented by the subclasses."""
 
     def interpolate(self, interp_kind="nearest"):
-        """screen.py:108-154; phase-only screens need no interpolation."""
+        """Put the slow amplitudes on the fast-phase time / frequency grid
+        (screen.py:108-154): interpolation in log10 space along time, then
+        frequency, extrapolating at the ends; KL screens already hold log10
+        values (``log_amps``), tessellated ones hold amplitudes."""
         if self.phase_only:
             return
-        raise NotImplementedError("amplitude (gain) screens: next row of the build")
+        vals = np.asarray(self.vals_amp)
+        n_t, n_f = np.shape(self.vals_ph)[:2]
+        if len(self.times_amp) == 1:
+            shape = list(vals.shape)
+            shape[0], shape[1] = n_t, n_f
+            self.vals_amp = np.resize(vals, shape)
+            return
+        logvals = vals if self.log_amps else np.log10(vals)
+        if vals.shape[0] != n_t:
+            logvals = resample_axis(self.times_amp, logvals, self.times_ph, 0,
+                                    interp_kind)
+        if vals.shape[1] != n_f:
+            logvals = resample_axis(self.freqs_amp, logvals, self.freqs_ph, 1,
+                                    interp_kind)
+        self.vals_amp = logvals if self.log_amps else 10 ** logvals
 
     def grid_size(self, cellsize_deg):
         return (int(np.ceil(self.width_ra / cellsize_deg)),

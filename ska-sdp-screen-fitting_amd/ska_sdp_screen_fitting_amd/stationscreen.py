@@ -13,7 +13,7 @@ import logging
 import numpy as np
 
 from . import geometry
-from ._lib import SF_SCREEN_PHASE, SF_SCREEN_TEC, get_context
+from ._lib import SF_SCREEN_AMPLITUDE, SF_SCREEN_PHASE, SF_SCREEN_TEC, get_context
 
 log = logging.getLogger("ska_sdp_screen_fitting_amd.stationscreen")
 
@@ -66,7 +66,10 @@ def _device_fit(phase, weight, pp, st_order, screen_type, niter, nsigma,
 def run(soltab, outsoltab, order=12, beta=5.0 / 3.0, niter=2, nsigma=5.0,
         ref_ant=-1, scale_order=True, scale_dist=None, min_order=5,
         adjust_order=True, ncpu=0, device=0):
-    """Fit station screens to a phase or tec soltab (stationscreen.py:858).
+    """Fit station screens to a phase, tec or amplitude soltab
+    (stationscreen.py:858).  Amplitude screens are fitted to log10 of the
+    amplitudes, per polarization, with one outlier sigma per (station, freq)
+    block (stationscreen.py:535-548, 669-700).
 
     Writes ``outsoltab`` (white KL coefficients, weights after flagging) and
     ``outsoltab + "resid"`` (residuals, orders as weights) into the soltab's
@@ -77,11 +80,7 @@ def run(soltab, outsoltab, order=12, beta=5.0 / 3.0, niter=2, nsigma=5.0,
     """
     del ncpu
     screen_type = soltab.get_type()
-    if screen_type not in ("phase", "tec"):
-        if screen_type == "amplitude":
-            raise NotImplementedError(
-                "amplitude screens (stationscreen.py:535-548, Q6 block "
-                "coupling) are not implemented on the GPU path yet")
+    if screen_type not in ("phase", "tec", "amplitude"):
         log.error('Screens can only be fit to soltabs of type "phase", '
                   '"tec", or "amplitude".')
         return 1
@@ -118,7 +117,8 @@ def run(soltab, outsoltab, order=12, beta=5.0 / 3.0, niter=2, nsigma=5.0,
     r_0 = 100
     pp, mid_ra, mid_dec = geometry.piercepoints(source_positions)
 
-    stype = SF_SCREEN_PHASE if screen_type == "phase" else SF_SCREEN_TEC
+    stype = {"phase": SF_SCREEN_PHASE, "tec": SF_SCREEN_TEC,
+             "amplitude": SF_SCREEN_AMPLITUDE}[screen_type]
     coef = np.zeros(val.shape)
     resid = np.zeros(val.shape)
     w_out = np.zeros(weight.shape, dtype=np.float32)

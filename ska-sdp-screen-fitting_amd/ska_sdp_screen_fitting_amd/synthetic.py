@@ -123,3 +123,34 @@ def make_solutions(n_ant, n_time, n_freq, n_dir, seed=20260, flag_frac=0.01,
                        dir_radec=dir_radec,
                        meta=dict(seed=seed, n_ant_total=n_ant_total,
                                  ant_offset=ant_offset))
+
+
+def make_amplitudes(sol, n_time=None, n_freq=None, seed=20261, flag_frac=0.01,
+                    outlier_frac=0.005, rms_log=0.05):
+    """Synthetic XX/YY amplitude soltab ([time, freq, ant, dir, pol]) on a
+    (possibly coarser) time / frequency grid spanning the phase grid: a smooth
+    log10-amplitude gradient across directions plus noise; outliers get x3.
+    Stored in ``sol.amp_*`` (the slow-amplitude half of a "gain" solution)."""
+    T, F, A, D = sol.val.shape
+    n_time = n_time or T
+    n_freq = n_freq or F
+    rng = np.random.default_rng(seed)
+    t = np.linspace(sol.times[0], sol.times[-1], n_time)
+    f = np.linspace(sol.freqs[0], sol.freqs[-1], n_freq)
+    ra = sol.dir_radec[:, 0].astype(np.float64)
+    de = sol.dir_radec[:, 1].astype(np.float64)
+    basis = np.stack([ra - ra.mean(), de - de.mean()], axis=0)
+    basis /= np.sqrt((basis ** 2).mean(axis=1, keepdims=True)) + 1e-30
+    coeff = rng.normal(0.0, rms_log, size=(n_time, n_freq, A, 2, 2))
+    logamp = np.einsum("tfapk,kd->tfadp", coeff, basis)
+    logamp += rng.normal(0.0, rms_log / 5, size=logamp.shape)
+    amp = 10.0 ** logamp
+    out = rng.random(amp.shape) < outlier_frac
+    amp[out] *= 3.0
+    w = np.ones(amp.shape, np.float32)
+    w[rng.random(amp.shape) < flag_frac] = 0.0
+    sol.amp_val = amp
+    sol.meta["amp_weight"] = w
+    sol.meta["amp_times"] = t
+    sol.meta["amp_freqs"] = f
+    return sol

@@ -144,9 +144,9 @@ class VoronoiScreen(Screen):
         self._dev_cache = None
 
     def fit(self):
-        """Reference the phases to one station (voronoi_screen.py:57-102)."""
-        if not self.phase_only:
-            raise NotImplementedError("gain (amplitude) tessellated screens: next row")
+        """Reference the phases to one station (voronoi_screen.py:57-102);
+        gain solutions also keep the raw XX / YY amplitudes
+        [time, freq, ant, dir, pol] for interpolation."""
         h5 = H5parm(self.input_h5parm_filename)
         solset = h5.get_solset(self.input_solset_name)
         st = solset.get_soltab(self.input_phase_soltab_name)
@@ -156,8 +156,17 @@ class VoronoiScreen(Screen):
         self.vals_ph = vals
         self.times_ph = np.asarray(st.time)
         self.freqs_ph = np.asarray(st.freq)
-        self.vals_amp = None  # ones (phase only)
-        self.times_amp, self.freqs_amp = self.times_ph, self.freqs_ph
+        if self.phase_only:
+            self.vals_amp = None  # ones (phase only)
+            self.times_amp, self.freqs_amp = self.times_ph, self.freqs_ph
+        else:
+            sta = solset.get_soltab(self.input_amplitude_soltab_name)
+            names = sta.get_axes_names()
+            order = [names.index(a) for a in ("time", "freq", "ant", "dir", "pol")]
+            self.log_amps = False
+            self.vals_amp = np.transpose(np.asarray(sta.val, np.float64), order)
+            self.times_amp = np.asarray(sta.time)
+            self.freqs_amp = np.asarray(sta.freq)
         self.source_names = st.dir
         self.source_dict = solset.get_source()
         self.source_positions = [self.source_dict[s] for s in self.source_names]
@@ -200,8 +209,9 @@ class VoronoiScreen(Screen):
         return self._dev_cache
 
     def eval_device(self, ph_dev, out_dev, smooth_pix=0.0,
-                    flags=SF_EVAL_NAN_SCRUB):
-        """device [S, D] referenced phases -> device [S, 4, ny, nx]."""
+                    flags=SF_EVAL_NAN_SCRUB, amp_xx=None, amp_yy=None):
+        """device [S, D] referenced phases (and optional XX / YY amplitudes,
+        device [S, D]) -> device [S, 4, ny, nx]."""
         import torch
         dev, lab = self._device()
         ny, nx = self.data_rasertize_template.shape
@@ -209,21 +219,28 @@ class VoronoiScreen(Screen):
         ctx = get_context(self.device)
         with torch.cuda.device(dev):
             ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
-            ctx.tess_fill(lab, nx, ny, ph_dev, D, S, out_dev,
-                          smooth_pix=smooth_pix, flags=flags)
+            ctx.tess_fill(lab, nx, ny, ph_dev, D, S, out_dev, amp_xx=amp_xx,
+                          amp_yy=amp_yy, smooth_pix=smooth_pix, flags=flags)
         return out_dev
 
-    def eval_host(self, phase, smooth_pix=0.0):
-        """[..., D] referenced phases -> float32 [..., 4, ny, nx] (gather +
-        optional Gaussian smoothing) on the GPU."""
+    def _upload(self, a):
         import torch
         dev, _ = self._device()
-        phase = np.ascontiguousarray(phase, np.float64)
-        lead = phase.shape[:-1]
+        a = np.ascontiguousarray(a, np.float64)
+        return torch.from_numpy(a.reshape(-1, a.shape[-1])).to(dev)
+
+    def eval_host(self, phase, smooth_pix=0.0, amp_xx=None, amp_yy=None):
+        """[..., D] referenced phases (optional amplitudes) -> float32
+        [..., 4, ny, nx] (gather + optional Gaussian smoothing) on the GPU."""
+        import torch
+        dev, _ = self._device()
+        lead = np.shape(phase)[:-1]
         ny, nx = self.data_rasertize_template.shape
-        ph = torch.from_numpy(phase.reshape(-1, phase.shape[-1])).to(dev)
+        ph = self._upload(phase)
+        axx = None if amp_xx is None else self._upload(amp_xx)
+        ayy = None if amp_yy is None else self._upload(amp_yy)
         out = torch.empty((ph.shape[0], 4, ny, nx), dtype=torch.float32, device=dev)
-        self.eval_device(ph, out, smooth_pix)
+        self.eval_device(ph, out, smooth_pix, amp_xx=axx, amp_yy=ayy)
         return out.cpu().numpy().reshape(lead + (4, ny, nx))
 
     def make_matrix(self, t_start_index, t_stop_index, freq_ind, stat_ind,
@@ -232,8 +249,13 @@ class VoronoiScreen(Screen):
         del ncpu
         if self.data_rasertize_template is None:
             self.make_rasertize_template(cellsize_deg, out_dir)
-        ph = self.vals_ph[t_start_index:t_stop_index, freq_ind, stat_ind, :]
-        return self.eval_host(ph).astype(np.float64)
+        sl = np.s_[t_start_index:t_stop_index, freq_ind, stat_ind, :]
+        ph = self.vals_ph[sl]
+        if self.phase_only:
+            return self.eval_host(ph).astype(np.float64)
+        amp = np.asarray(self.vals_amp)[sl]
+        return self.eval_host(ph, amp_xx=amp[..., 0],
+                              amp_yy=amp[..., 1]).astype(np.float64)
 
     def write(self, out_dir, cellsize_deg, smooth_pix=0, ncpu=0):
         if self.data_rasertize_template is None:
@@ -252,8 +274,11 @@ class VoronoiScreen(Screen):
         per_slot = 16 * nx * ny
         row_bytes = n_f * n_a * per_slot
         rows = min(max(1, int(max_batch_bytes // row_bytes)), g_stop - g_start)
-        ph = torch.from_numpy(np.ascontiguousarray(
-            self.vals_ph[g_start:g_stop].reshape(-1, D), np.float64)).to(dev)
+        ph = self._upload(self.vals_ph[g_start:g_stop])
+        axx = ayy = None
+        if not self.phase_only:
+            amp = np.asarray(self.vals_amp)[g_start:g_stop]
+            axx, ayy = self._upload(amp[..., 0]), self._upload(amp[..., 1])
         pipe = PinnedPipeline(torch, dev, rows * row_bytes)
         try:
             for t0 in range(g_start, g_stop, rows):
@@ -262,7 +287,9 @@ class VoronoiScreen(Screen):
                 slot, buf = pipe.device_buffer((s1 - s0) * per_slot)
                 out = buf.view(torch.float32).view(s1 - s0, 4, ny, nx)
                 self.eval_device(ph[s0:s1], out, smooth_pix,
-                                 SF_EVAL_NAN_SCRUB | SF_EVAL_BIG_ENDIAN)
+                                 SF_EVAL_NAN_SCRUB | SF_EVAL_BIG_ENDIAN,
+                                 amp_xx=None if axx is None else axx[s0:s1],
+                                 amp_yy=None if ayy is None else ayy[s0:s1])
                 pipe.submit(slot, (s1 - s0) * per_slot, writer)
         finally:
             pipe.close()

@@ -1,0 +1,250 @@
+"""Gain (phase + slow XX/YY amplitude) screens, SURVEY.md §8(f) row 3.
+
+Golden vectors: tests/golden/gain12.npz, made by running the reference itself
+(tests/golden/make_golden_gain.py): the amplitude stationscreen.run exactly as
+KLScreen.fit calls it (kl_screen.py:96-125), Screen.interpolate
+(screen.py:108-154) and KLScreen.make_matrix with amplitudes
+(kl_screen.py:319-378).  The tessellated gain planes are checked against the
+oracle restatement (the reference's tessellated path needs shapely).
+
+Tolerances: amplitude coefficients |d| <= 1e-8 x max(1, |coef|max) (as the
+phase fit); orders and flagged weights identical; interpolation exact (a row
+gather); gain planes |d| <= 1e-6 x max(1, amplitude) with fp32 sincos / exp10
+(2e-6 fast path).
+"""
+
+import os
+
+import numpy as np
+import pytest
+
+from conftest import FIELD, GOLDEN, load_golden
+from oracle import kl as okl
+from oracle import voronoi as ov
+
+
+@pytest.fixture(scope="module")
+def gain():
+    return load_golden("gain12")
+
+
+# ---------------------------------------------------------------- CPU: oracle
+
+def test_oracle_amplitude_fit_vs_reference(gain):
+    g = gain
+    r = okl.run_amplitude(g["amp_val"], g["amp_weight"], g["piercepoints"],
+                          int(g["amp_order"]))
+    np.testing.assert_array_equal(r["orders"], g["amp_orders"])
+    np.testing.assert_array_equal(r["w_out"], g["amp_w_out"])
+    scale = max(1.0, np.abs(g["amp_coef"]).max())
+    np.testing.assert_allclose(r["coef"], g["amp_coef"], rtol=0, atol=1e-10 * scale)
+    np.testing.assert_allclose(r["resid"], g["amp_resid"], rtol=0, atol=1e-10)
+    # the block-coupled sigma flags something beyond the input flags
+    assert (g["amp_w_out"] == 0).sum() > (g["amp_weight"] == 0).sum()
+
+
+def test_oracle_interpolation_vs_reference(gain):
+    g = gain
+    got = okl.interpolate_nearest(g["amp_coef"], g["amp_times"], g["amp_freqs"],
+                                  g["times"], g["freqs"])
+    np.testing.assert_array_equal(got, g["amp_interp"])
+
+
+def test_oracle_gain_planes_vs_reference(gain):
+    g = gain
+    cpix = okl.cpix_matrix(g["piercepoints"], g["x17"], g["y17"])
+    for k, (f, a) in enumerate(g["pairs"]):
+        ph = okl.eval_phase_screens(g["coef"][:, f, a, :], cpix)
+        ax = 10 ** okl.eval_phase_screens(g["amp_interp"][:, f, a, :, 0], cpix)
+        ay = 10 ** okl.eval_phase_screens(g["amp_interp"][:, f, a, :, 1], cpix)
+        want = okl.eval_planes(ph, ax, ay).reshape(g["gain17"][k].shape)
+        np.testing.assert_allclose(want, g["gain17"][k], rtol=0, atol=1e-12)
+
+
+# ------------------------------------------------------ CPU: product host code
+
+def test_nearest_index_matches_scipy():
+    import scipy.interpolate as si
+    from ska_sdp_screen_fitting_amd.screen import nearest_index
+    rng = np.random.default_rng(5)
+    src = np.sort(rng.random(7)) * 10
+    # ties at exact midpoints, points outside both ends, duplicates
+    dst = np.concatenate([(src[1:] + src[:-1]) / 2.0, [-3.0, 42.0], src,
+                          rng.random(50) * 12 - 1])
+    vals = np.arange(7, dtype=np.float64)
+    want = si.interp1d(src, vals, kind="nearest", fill_value="extrapolate")(dst)
+    np.testing.assert_array_equal(vals[nearest_index(src, dst)], want)
+
+
+def test_screen_interpolate_vs_reference(gain):
+    from ska_sdp_screen_fitting_amd.screen import Screen
+    g = gain
+    s = Screen("x", None, None, 0.0, 0.0, 1.0, 1.0, amplitude_soltab_name="amp")
+    s.vals_ph, s.times_ph, s.freqs_ph = g["coef"], g["times"], g["freqs"]
+    s.vals_amp, s.times_amp, s.freqs_amp = g["amp_coef"], g["amp_times"], g["amp_freqs"]
+    s.log_amps = True
+    s.interpolate()
+    np.testing.assert_array_equal(s.vals_amp, g["amp_interp"])
+    # tessellated screens interpolate raw amplitudes through log10 space
+    s.vals_amp, s.log_amps = 10 ** g["amp_coef"], False
+    s.interpolate()
+    np.testing.assert_allclose(s.vals_amp, 10 ** g["amp_interp"], rtol=1e-14)
+    # a single amplitude time: repeated onto the phase grid
+    s.vals_amp = g["amp_coef"][:1, :1]
+    s.times_amp = g["amp_times"][:1]
+    s.interpolate()
+    assert s.vals_amp.shape == g["amp_interp"].shape
+
+
+# ------------------------------------------------------------------- GPU
+
+def _torch_dev():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch, torch.device("cuda", 0)
+
+
+def _ctx(torch, dev):
+    from ska_sdp_screen_fitting_amd import get_context
+    c = get_context(0)
+    c.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    return c
+
+
+@pytest.mark.gpu
+def test_amplitude_fit_vs_reference(gain):
+    from ska_sdp_screen_fitting_amd._lib import SF_SCREEN_AMPLITUDE
+    torch, dev = _torch_dev()
+    ctx = _ctx(torch, dev)
+    g = gain
+    ctx.set_basis(g["piercepoints"])
+    T, F, A, D, P = g["amp_val"].shape
+    order = int(g["amp_order"])
+    scale = max(1.0, np.abs(g["amp_coef"]).max())
+    for p in range(P):
+        v = torch.from_numpy(np.ascontiguousarray(g["amp_val"][..., p])).to(dev)
+        w = torch.from_numpy(np.ascontiguousarray(g["amp_weight"][..., p])).to(dev)
+        coef, resid, w_out = torch.empty_like(v), torch.empty_like(v), torch.empty_like(w)
+        orders = torch.empty((T, F, A), dtype=torch.int32, device=dev)
+        ctx.fit(v, w, T, F, A, [order] * A, screen_type=SF_SCREEN_AMPLITUDE,
+                niter=3, ref_ant=-1, coef=coef, resid=resid, w_out=w_out,
+                order_out=orders)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(orders.cpu().numpy(), g["amp_orders"][..., p])
+        np.testing.assert_array_equal(w_out.cpu().numpy(), g["amp_w_out"][..., p])
+        np.testing.assert_allclose(coef.cpu().numpy(), g["amp_coef"][..., p],
+                                   rtol=0, atol=1e-8 * scale)
+        np.testing.assert_allclose(resid.cpu().numpy(), g["amp_resid"][..., p],
+                                   rtol=0, atol=1e-8)
+
+
+@pytest.mark.gpu
+def test_amplitude_fit_vs_oracle_larger():
+    """More stations / times, NaN blocks and all-flagged blocks (skipped)."""
+    from ska_sdp_screen_fitting_amd import geometry
+    from ska_sdp_screen_fitting_amd._lib import SF_SCREEN_AMPLITUDE
+    from ska_sdp_screen_fitting_amd.synthetic import make_amplitudes, make_solutions
+    torch, dev = _torch_dev()
+    ctx = _ctx(torch, dev)
+    s = make_solutions(n_ant=6, n_time=4, n_freq=2, n_dir=20, seed=7)
+    make_amplitudes(s, seed=8, flag_frac=0.05, outlier_frac=0.03)
+    amp = s.amp_val.copy()
+    wt = s.meta["amp_weight"].copy()
+    amp[:, 1, 2] = np.nan          # an all-NaN (freq, station) block
+    wt[:, 0, 4] = 0.0              # an all-flagged block
+    pp, _, _ = geometry.piercepoints(s.dir_radec)
+    order = 10
+    want = okl.run_amplitude(amp, wt, pp, order)
+    ctx.set_basis(pp)
+    T, F, A, D, P = amp.shape
+    for p in range(P):
+        v = torch.from_numpy(np.ascontiguousarray(amp[..., p])).to(dev)
+        w = torch.from_numpy(np.ascontiguousarray(wt[..., p])).to(dev)
+        coef, resid, w_out = torch.zeros_like(v), torch.zeros_like(v), torch.empty_like(w)
+        orders = torch.zeros((T, F, A), dtype=torch.int32, device=dev)
+        ctx.fit(v, w, T, F, A, [order] * A, screen_type=SF_SCREEN_AMPLITUDE,
+                niter=3, ref_ant=-1, coef=coef, resid=resid, w_out=w_out,
+                order_out=orders)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(orders.cpu().numpy(), want["orders"][..., p])
+        np.testing.assert_array_equal(w_out.cpu().numpy(), want["w_out"][..., p])
+        np.testing.assert_allclose(coef.cpu().numpy(), want["coef"][..., p],
+                                   rtol=0, atol=1e-8 * max(1.0, np.abs(want["coef"]).max()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fast", [False, True])
+def test_gain_eval_vs_reference(gain, fast):
+    from ska_sdp_screen_fitting_amd._lib import (SF_EVAL_FAST_SINCOS,
+                                                 SF_EVAL_NAN_SCRUB)
+    torch, dev = _torch_dev()
+    ctx = _ctx(torch, dev)
+    g = gain
+    ctx.set_basis(g["piercepoints"])
+    ctx.set_grid(g["x17"], g["y17"])
+    flags = SF_EVAL_NAN_SCRUB | (SF_EVAL_FAST_SINCOS if fast else 0)
+    tol = 2e-6 if fast else 1e-6
+    for k, (f, a) in enumerate(g["pairs"]):
+        up = [torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in
+              (g["coef"][:, f, a, :], g["amp_interp"][:, f, a, :, 0],
+               g["amp_interp"][:, f, a, :, 1])]
+        S = up[0].shape[0]
+        out = torch.full((S, 4, 17, 17), -7.0, dtype=torch.float32, device=dev)
+        ctx.eval_gain(up[0], up[1], up[2], S, out, S, flags)
+        torch.cuda.synchronize()
+        ref = g["gain17"][k]
+        amp = np.maximum(1.0, np.abs(ref))
+        err = np.abs(out.cpu().numpy() - ref) / amp
+        assert err.max() <= tol, err.max()
+
+
+@pytest.mark.gpu
+def test_make_aterm_image_gain_kl(tmp_path, gain):
+    """make_aterm_image on a gain solution set (soltab "gain000" -> phase000
+    + amplitude000), FITS cube vs the reference's make_matrix output."""
+    _torch_dev()
+    from ska_sdp_screen_fitting_amd import fits as sffits
+    from ska_sdp_screen_fitting_amd.make_aterm_images import make_aterm_image
+    g = gain
+    outroot = str(tmp_path / "gain")
+    make_aterm_image(os.path.join(GOLDEN, "gain12.npz"), soltabname="gain000",
+                     screen_type="kl", outroot=outroot,
+                     bounds_deg=[124.565, 66.165, 127.895, 62.835],
+                     bounds_mid_deg=[126.23, 64.50], skymodel=None,
+                     padding_fraction=0, cellsize_deg=0.2, ncpu=0)
+    _, cube = sffits.read_cube(outroot + "_0.fits")
+    assert cube.shape == (8, 3, 5, 4, 17, 17)
+    for k, (f, a) in enumerate(g["pairs"]):
+        ref = g["gain17"][k]
+        err = np.abs(cube[:, f, a] - ref) / np.maximum(1.0, np.abs(ref))
+        assert err.max() <= 2e-6, (k, err.max())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("smooth", [0.0, 1.3])
+def test_tess_gain_vs_oracle(gain, smooth):
+    from ska_sdp_screen_fitting_amd.voronoi_screen import tessellation_template
+    torch, dev = _torch_dev()
+    ctx = _ctx(torch, dev)
+    g = gain
+    radec = np.rad2deg(g["dir_radec"].astype(np.float64))
+    lab, _ = tessellation_template(radec, FIELD["rad"], FIELD["dec"],
+                                   FIELD["width"], 0.05)
+    ref = int(g["ref_ant"])
+    ph = (g["val"] - g["val"][:, :, ref:ref + 1, :]).reshape(-1, 12)
+    amp = 10 ** g["amp_interp"].reshape(-1, 12, 2)
+    axx, ayy = np.ascontiguousarray(amp[..., 0]), np.ascontiguousarray(amp[..., 1])
+    ny, nx = lab.shape
+    S = ph.shape[0]
+    d = [torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (ph, axx, ayy)]
+    lab_d = torch.from_numpy(np.ascontiguousarray(lab, np.int32)).to(dev)
+    out = torch.full((S, 4, ny, nx), -5.0, dtype=torch.float32, device=dev)
+    ctx.tess_fill(lab_d, nx, ny, d[0], 12, S, out, amp_xx=d[1], amp_yy=d[2],
+                  smooth_pix=smooth)
+    torch.cuda.synchronize()
+    want = ov.gather_planes(lab, ph, axx, ayy)
+    if smooth > 0:
+        want = ov.smooth(want, smooth)
+    np.testing.assert_allclose(out.cpu().numpy(), want, rtol=0,
+                               atol=1e-6 * max(1.0, np.abs(want).max()))
