@@ -446,6 +446,43 @@ def run_amplitude(val, weight, pp, order, r_0=100.0, beta=5.0 / 3.0, niter=3,
     return dict(coef=coef, resid=resid, w_out=w_out, orders=orders)
 
 
+def run_soltab(val, weight, ant_pos, pp, ref_ant, order, screen_type,
+               r_0=100.0, beta=5.0 / 3.0, niter=2, nsigma=5.0, min_order=5,
+               scale_order=True, adjust_order=True):
+    """stationscreen.run (:858-1161) for one polarization [time, freq, ant,
+    dir] of any screen type, block by block through process_station_block:
+    referencing with the Q15 precedence (:993-996; tec with ref_ant == -1
+    subtracts the LAST station), the reference-station skip for phase / tec
+    (:818-820) and the all-NaN / all-flagged skip (:822-827)."""
+    val = np.array(val, dtype=np.float64)
+    weight = np.asarray(weight, dtype=np.float32)
+    nt, nf, na, nd = val.shape
+    if ref_ant != -1 and screen_type == "phase" or screen_type == "tec":
+        val = val - val[:, :, ref_ant:ref_ant + 1 if ref_ant != -1 else None, :]
+    st_order = station_orders(ant_pos, ref_ant, order, min_order, scale_order)
+    basis = Basis(pp, r_0, beta)
+    coef = np.zeros_like(val)
+    resid = np.zeros_like(val)
+    w_out = weight.copy()
+    orders = np.zeros((nt, nf, na), dtype=np.int32)
+    for f in range(nf):
+        for a in range(na):
+            if a == ref_ant and screen_type in ("phase", "tec"):
+                continue
+            v = val[:, f, a, :].T
+            w = weight[:, f, a, :].T
+            if np.all(np.isnan(v)) or np.all(w == 0):
+                continue
+            sc, rs, ww, oo = process_station_block(v, w, st_order[a], basis,
+                                                   screen_type, niter, nsigma,
+                                                   adjust_order)
+            coef[:, f, a] = sc.T
+            resid[:, f, a] = rs.T
+            w_out[:, f, a] = ww.T
+            orders[:, f, a] = oo.astype(np.int32)
+    return dict(coef=coef, resid=resid, w_out=w_out, orders=orders)
+
+
 def interpolate_nearest(vals, src_times, src_freqs, dst_times, dst_freqs):
     """screen.py:108-154 on log-amplitude coefficients: scipy interp1d
     (kind="nearest", fill_value="extrapolate") along time then frequency."""

@@ -1,0 +1,82 @@
+"""tec screens (stationscreen.py:858-1161 on a tec soltab) vs golden vectors
+from the reference itself (tests/golden/make_golden_tec.py): the referenced
+case and the ref_ant == -1 case where the operator-precedence quirk Q15
+references tec to the last station; niter=3 (block-coupled outlier sigma,
+quirk Q6 -- one sigma per (station, freq) block), tiny weights (the pinv(G)
+branch) and an all-NaN block.
+
+Tolerances as the phase fit: coefficients / residuals |d| <= 1e-8 x
+max(1, |coef|max); orders and flagged weights identical.
+"""
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from oracle import kl as okl
+
+CASES = ("ref", "noref")
+
+
+@pytest.fixture(scope="module")
+def tec():
+    return load_golden("tec14")
+
+
+def _check(g, case, coef, resid, w_out, orders, tol):
+    np.testing.assert_array_equal(orders, g[f"{case}_orders"])
+    np.testing.assert_array_equal(w_out, g[f"{case}_w_out"])
+    scale = max(1.0, np.abs(g[f"{case}_coef"]).max())
+    np.testing.assert_allclose(coef, g[f"{case}_coef"], rtol=0, atol=tol * scale)
+    np.testing.assert_allclose(resid, g[f"{case}_resid"], rtol=0, atol=tol)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_oracle_tec_vs_reference(tec, case):
+    g = tec
+    r = okl.run_soltab(g["val"], g["weight"], g["ant_pos"], g["piercepoints"],
+                       int(g[f"{case}_ref_ant"]), int(g["order"]), "tec",
+                       niter=int(g["niter"]))
+    _check(g, case, r["coef"], r["resid"], r["w_out"], r["orders"], 1e-10)
+
+
+def test_oracle_block_driver_equals_slot_driver():
+    """run_soltab (block restatement) == run_phase (per-slot restatement) for
+    phase, where the two are equivalent (oracle/kl.py header)."""
+    g = load_golden("synth20")
+    args = (g["val"], g["weight"], g["ant_pos"], g["piercepoints"],
+            int(g["ref_ant"]), int(g["order"]))
+    a = okl.run_soltab(*args, "phase")
+    b = okl.run_phase(*args)
+    for k in ("orders", "w_out"):
+        np.testing.assert_array_equal(a[k], b[k])
+    np.testing.assert_allclose(a["coef"], b["coef"], rtol=0, atol=1e-12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES)
+def test_tec_fit_vs_reference(tec, case):
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from ska_sdp_screen_fitting_amd import get_context
+    from ska_sdp_screen_fitting_amd._lib import SF_SCREEN_TEC
+    from ska_sdp_screen_fitting_amd.stationscreen import station_orders
+    g = tec
+    dev = torch.device("cuda", 0)
+    ctx = get_context(0)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    ctx.set_basis(g["piercepoints"])
+    ref = int(g[f"{case}_ref_ant"])
+    st = station_orders(g["ant_pos"], ref, int(g["order"]))
+    T, F, A, D = g["val"].shape
+    v = torch.from_numpy(np.ascontiguousarray(g["val"])).to(dev)
+    w = torch.from_numpy(np.ascontiguousarray(g["weight"])).to(dev)
+    coef, resid = torch.zeros_like(v), torch.zeros_like(v)
+    w_out = torch.empty_like(w)
+    orders = torch.zeros((T, F, A), dtype=torch.int32, device=dev)
+    ctx.fit(v, w, T, F, A, st, screen_type=SF_SCREEN_TEC, niter=int(g["niter"]),
+            ref_ant=ref, coef=coef, resid=resid, w_out=w_out, order_out=orders)
+    torch.cuda.synchronize()
+    _check(g, case, coef.cpu().numpy(), resid.cpu().numpy(), w_out.cpu().numpy(),
+           orders.cpu().numpy(), 1e-8)
