@@ -7,10 +7,12 @@ make_soltab`` :460-799, ``Soltab`` axis access :1306-1324).
 
 Storage backends:
 
-* ``.h5`` / ``.h5parm`` through h5py when h5py is importable (read only; the
-  LoSoTo layout: ``/<solset>/<soltab>/{val,weight,<axis>}`` with an ``AXES``
-  attribute, ``/<solset>/antenna`` and ``/<solset>/source`` tables);
-* ``.npz`` produced by ``tools/h5parm_to_npz.py`` (the GPU box has no h5py):
+* ``.h5`` / ``.h5parm`` through the built-in read-only HDF5 reader
+  (``hdf5.py``; neither PyTables nor h5py is needed) -- the LoSoTo / DP3
+  layout: ``/<solset>/<soltab>/{val,weight,<axis>}`` with an ``AXES``
+  attribute, ``TITLE`` = soltab type, ``/<solset>/antenna`` and
+  ``/<solset>/source`` compound tables;
+* ``.npz`` produced by ``tools/h5parm_to_npz.py``:
   keys ``val weight times freqs dir_names ant_names dir_radec ant_pos``
   (+ optional ``soltab``/``solset`` names and ``pol``/``amp_*`` arrays).
 
@@ -108,6 +110,11 @@ class H5parm:
     def close(self):
         pass
 
+    def save(self, path, weight_dtype=np.float16):
+        """Write every solset -- including soltabs made by
+        ``stationscreen.run`` -- to a new H5parm file (see write_h5parm)."""
+        write_h5parm(path, list(self.solsets.values()), weight_dtype)
+
     def get_solset(self, name="sol000"):
         if name not in self.solsets:
             raise KeyError(f"solset {name!r} not in {self.path}")
@@ -139,36 +146,98 @@ class H5parm:
         self.solsets[solset_name] = ss
 
     def _load_h5(self, path):
-        try:
-            import h5py
-        except ImportError as exc:  # the GPU box has no h5py
-            raise ImportError(
-                "reading .h5 H5parm files needs h5py; convert with "
-                "tools/h5parm_to_npz.py and pass the .npz") from exc
-        with h5py.File(path, "r") as f:
-            for ssn in f:
+        """LoSoTo / DP3 layout through the built-in HDF5 reader (hdf5.py)."""
+        from . import hdf5
+
+        def text(v):
+            v = v.decode() if isinstance(v, bytes) else str(v)
+            return v
+
+        with hdf5.File(path) as f:
+            for ssn in f.keys():
                 g = f[ssn]
-                ants = g["antenna"][:]
-                srcs = g["source"][:]
-                ss = Solset(ssn, [a["name"].decode() for a in ants],
-                            [a["position"] for a in ants],
-                            [s["name"].decode() for s in srcs],
-                            [s["dir"] for s in srcs])
-                for stn in g:
+                if not isinstance(g, hdf5.Group) or "antenna" not in g:
+                    continue
+                ants = g["antenna"][()]
+                srcs = g["source"][()]
+                ss = Solset(ssn, [text(a) for a in ants["name"]],
+                            np.asarray(ants["position"]),
+                            [text(s) for s in srcs["name"]],
+                            np.asarray(srcs["dir"]))
+                for stn in g.keys():
                     if stn in ("antenna", "source"):
                         continue
                     st = g[stn]
-                    axes = st["val"].attrs["AXES"].decode().split(",")
+                    if not isinstance(st, hdf5.Group) or "val" not in st:
+                        continue
+                    val = st["val"]
+                    axes = text(val.attrs["AXES"]).split(",")
                     avals = []
                     for a in axes:
-                        v = st[a][:]
-                        if v.dtype.kind == "S":
-                            v = v.astype(str)
+                        v = st[a][()]
+                        if v.dtype.kind in "SO":
+                            v = np.array([text(x) for x in v])
                         avals.append(v)
-                    title = st.attrs.get("TITLE", b"").decode()
-                    ss.soltabs[stn] = Soltab(stn, title, axes, avals,
-                                             st["val"][:], st["weight"][:], ss)
+                    title = text(st.attrs.get("TITLE", b""))
+                    extra = {k: v for k, v in st.attrs.items()
+                             if k not in ("TITLE", "CLASS", "VERSION",
+                                          "parmdb_type", "h5parm_version")}
+                    tab = Soltab(stn, title, axes, avals,
+                                 np.asarray(val[()], np.float64),
+                                 np.asarray(st["weight"][()], np.float32), ss,
+                                 attrs=extra)
+                    if "piercepoint" in st:
+                        tab.piercepoint = st["piercepoint"][()]
+                    ss.soltabs[stn] = tab
                 self.solsets[ssn] = ss
+
+
+def _bytes_array(values):
+    a = np.asarray(values)
+    return np.char.encode(a.astype(str), "utf8") if a.dtype.kind in "UO" else a
+
+
+def write_h5parm(path, solsets, weight_dtype=np.float16):
+    """Write solsets (``H5parm.solsets`` values) as a new H5parm file in the
+    LoSoTo layout PyTables reads (utils/h5parm.py:164-221 make_solset,
+    :509-640 make_soltab): per solset the ``antenna`` (name S16, position
+    f4[3]) and ``source`` (name S128, dir f4[2]) tables; per soltab a group
+    titled with the soltab type, one array per axis, ``val`` (f8) and
+    ``weight`` (f16 by default) with the ``AXES`` attribute, the soltab's
+    attributes (the screen soltabs' beta, r_0, height, midra, middec) and its
+    ``piercepoint`` array when set (stationscreen.py:1147-1157)."""
+    from .hdf5 import Writer
+    w = Writer()
+    for ss in solsets:
+        root = "/" + ss.name
+        w.group_attrs(root, {"h5parm_version": b"1.0"})
+        ants = ss.get_ant()
+        at = np.zeros(len(ants), dtype=[("name", "S16"), ("position", "<f4", (3,))])
+        at["name"] = _bytes_array(list(ants))
+        at["position"] = np.array(list(ants.values()), np.float32).reshape(-1, 3)
+        w.dataset(root + "/antenna", at)
+        srcs = ss.get_source()
+        sr = np.zeros(len(srcs), dtype=[("name", "S128"), ("dir", "<f4", (2,))])
+        sr["name"] = _bytes_array(list(srcs))
+        sr["dir"] = np.array(list(srcs.values()), np.float32).reshape(-1, 2)
+        w.dataset(root + "/source", sr)
+        for name, st in ss.soltabs.items():
+            g = f"{root}/{name}"
+            attrs = {"TITLE": str(st.get_type()).encode(), "parmdb_type": b"",
+                     "h5parm_version": b"1.0"}
+            for k, v in st.attrs.items():
+                attrs[k] = np.float64(v) if np.isscalar(v) and not isinstance(v, (str, bytes)) else v
+            w.group_attrs(g, attrs)
+            axes = st.get_axes_names()
+            for a in axes:
+                w.dataset(f"{g}/{a}", _bytes_array(getattr(st, a)))
+            ax = ",".join(axes).encode()
+            w.dataset(g + "/val", np.asarray(st.val, np.float64), {"AXES": ax})
+            w.dataset(g + "/weight", np.asarray(st.weight).astype(weight_dtype),
+                      {"AXES": ax})
+            if st.piercepoint is not None:
+                w.dataset(g + "/piercepoint", np.asarray(st.piercepoint, np.float64))
+    w.save(path)
 
 
 def get_reference_station(soltab, max_ind=None):

@@ -268,3 +268,22 @@ def test_make_aterm_image_fixture_kl(tmp_path):
             for p, fn in ((0, np.cos), (1, np.sin), (2, np.cos), (3, np.sin)):
                 assert np.all(np.abs(cube[:, :, :, p, row, col] - fn(corr[..., i])) < 1e-1)
     assert n_in >= 5
+
+
+def test_make_aterm_image_from_h5parm_file(tmp_path):
+    """The same drop-in call on a DP3-layout .h5 (built-in HDF5 reader) gives
+    the same FITS cube as the .npz input."""
+    from ska_sdp_screen_fitting_amd import fits as sffits
+    from ska_sdp_screen_fitting_amd.make_aterm_images import make_aterm_image
+    cubes = []
+    for src, tag in ((os.path.join(GOLDEN, "fixture_kl.npz"), "npz"),
+                     (os.path.join(GOLDEN, "h5", "dp3_like.h5"), "h5")):
+        outroot = str(tmp_path / tag)
+        make_aterm_image(src, soltabname="phase000", screen_type="kl",
+                         outroot=outroot,
+                         bounds_deg=[124.565, 66.165, 127.895, 62.835],
+                         bounds_mid_deg=[126.23, 64.50],
+                         skymodel=os.path.join(GOLDEN, "skymodel.txt"),
+                         padding_fraction=0, cellsize_deg=0.2, ncpu=0)
+        cubes.append(sffits.read_cube(outroot + "_0.fits")[1])
+    np.testing.assert_array_equal(cubes[0], cubes[1])
