@@ -53,6 +53,15 @@ def parse():
     ap.add_argument("--no-fits", action="store_true",
                     help="skip the FITS-cube wall-clock leg (configs 1-2)")
     ap.add_argument("--cpu-workers", type=int, default=16)
+    ap.add_argument("--chunks", type=int, default=2,
+                    help="time chunks per step: the fit of chunk c+1 runs on a "
+                         "second stream while chunk c is evaluated (1 = fit "
+                         "then eval, serialised)")
+    ap.add_argument("--reserve-cus", type=int, default=16,
+                    help="compute units the eval stream leaves to the fit "
+                         "stream (pipelined mode)")
+    ap.add_argument("--fit-priority", type=int, default=1,
+                    help="1: fit stream at high priority (pipelined mode)")
     ap.add_argument("--eval-only", action="store_true",
                     help="time only sf_kl_eval (profiling)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
@@ -209,43 +218,100 @@ def main():
     flags = (SF_EVAL_NAN_SCRUB | SF_EVAL_NT_STORES
              | (0 if args.precise_sincos else SF_EVAL_FAST_SINCOS))
 
-    def fit():
-        ctx.fit(phase, weight, T, F, A, setup["st_order"], niter=2,
-                nsigma=5.0, adjust_order=True, ref_ant=setup["ref_ant"],
-                coef=coef, resid=resid, w_out=w_out, order_out=order_out,
-                ant_offset=setup["ant_offset"], ref_phase=refph)
+    # time chunks (the solution layout is time-major, so a chunk is a
+    # contiguous slice of every array); phase slots are independent, so the
+    # fit of one chunk can run while the previous chunk is evaluated
+    n_chunks = max(1, min(args.chunks, T))
+    bounds = [(T * c // n_chunks, T * (c + 1) // n_chunks) for c in range(n_chunks)]
+    # the eval saturates HBM without every CU: its stream leaves
+    # --reserve-cus compute units (spread over the XCDs) to the fit stream, so
+    # the fit of the next chunk is not starved by queued eval workgroups
+    fit_stream = stream
+    if n_chunks > 1:
+        fit_stream = torch.cuda.Stream(dev, priority=-1 if args.fit_priority else 0)
+        if args.reserve_cus > 0:
+            n_cu = ctx.device_cus()
+            step = max(1, n_cu // args.reserve_cus)
+            # k*step + k%8: one per XCD whether CUs are numbered XCD-major
+            # or interleaved across the 8 XCDs
+            reserved = [min(n_cu - 1, k * step + k % 8) for k in range(args.reserve_cus)]
+            stream = torch.cuda.ExternalStream(ctx.stream_create(reserved), device=dev)
 
-    def evaluate():
-        ctx.eval(coef, S, out, ring, flags)
+    def fit(c):
+        t0, t1 = bounds[c]
+        ctx.set_stream(fit_stream.cuda_stream)
+        ctx.fit(phase[t0:t1], weight[t0:t1], t1 - t0, F, A, setup["st_order"],
+                niter=2, nsigma=5.0, adjust_order=True, ref_ant=setup["ref_ant"],
+                coef=coef[t0:t1], resid=resid[t0:t1], w_out=w_out[t0:t1],
+                order_out=order_out[t0:t1], ant_offset=setup["ant_offset"],
+                ref_phase=refph[t0:t1])
 
-    for _ in range(args.warmup):
-        if not args.eval_only:
-            fit()
-        evaluate()
-    if args.eval_only and args.warmup == 0:
-        fit()
+    def evaluate(c):
+        t0, t1 = bounds[c]
+        ctx.set_stream(stream.cuda_stream)
+        ctx.eval(coef[t0:t1].reshape(-1, D), (t1 - t0) * F * A, out, ring, flags)
+
+    # work items in issue order: every step fits and evaluates all chunks;
+    # eval(c) waits for fit(c) (event), fit(c+1) is issued after eval(c) so
+    # it overlaps it; fit events bracket the fit stream, eval events the
+    # eval stream
+    def run_steps(n):
+        evs = []
+        items = [(k, c) for k in range(n) for c in range(n_chunks)]
+        if not items:
+            return evs
+        fit_done, eval_done = {}, {}
+
+        def issue_fit(i):
+            k, c = items[i]
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            if i >= n_chunks:
+                # coef[chunk c] is rewritten: wait for the previous step's
+                # eval of the same chunk (write-after-read across streams)
+                fit_stream.wait_event(eval_done[i - n_chunks])
+            e0.record(fit_stream)
+            if not args.eval_only:
+                fit(c)
+            e1.record(fit_stream)
+            fit_done[i] = (e0, e1)
+
+        issue_fit(0)
+        for i, (k, c) in enumerate(items):
+            stream.wait_event(fit_done[i][1])
+            e2 = torch.cuda.Event(enable_timing=True)
+            e3 = torch.cuda.Event(enable_timing=True)
+            e2.record(stream)
+            evaluate(c)
+            e3.record(stream)
+            eval_done[i] = e3
+            if i + 1 < len(items):
+                issue_fit(i + 1)
+            evs.append((fit_done[i][0], fit_done[i][1], e2, e3))
+        return evs
+
+    if args.eval_only:
+        for c in range(n_chunks):
+            fit(c)
+    run_steps(args.warmup)
     torch.cuda.synchronize(dev)
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        ev[k][0].record(stream)
-        if not args.eval_only:
-            fit()
-        ev[k][1].record(stream)
-        evaluate()
-        ev[k][2].record(stream)
+    ev = run_steps(args.steps)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    ctx.set_stream(stream.cuda_stream)
     fit_stats = ctx.fit_stats() if not args.eval_only else {}
-    t_fit = float(np.mean([a.elapsed_time(b) for a, b, _ in ev])) * 1e-3
-    t_eval = float(np.mean([b.elapsed_time(c) for _, b, c in ev])) * 1e-3
+    # per-step stage sums; per-launch eval duration for the roofline
+    t_fit = float(np.sum([a.elapsed_time(b) for a, b, _, _ in ev])) * 1e-3 / args.steps
+    eval_launch = [c_.elapsed_time(d_) for _, _, c_, d_ in ev]
+    t_eval = float(np.sum(eval_launch)) * 1e-3 / args.steps
+    t_eval_launch = float(np.mean(eval_launch)) * 1e-3
     tmax = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
     if world > 1:
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -256,15 +322,17 @@ def main():
     unit_err = float((chk[:, 0] ** 2 + chk[:, 1] ** 2 - 1).abs().max())
 
     if rank == 0:
-        algo_bytes = S * (16 * P + 8 * D)
-        achieved = algo_bytes / t_eval / 1e9
+        algo_bytes = S * (16 * P + 8 * D)  # SURVEY.md §8(d), per step
+        launch_bytes = algo_bytes / n_chunks  # per eval launch (equal chunks)
+        achieved = launch_bytes / t_eval_launch / 1e9
         traffic = None
         tpath = os.path.join(REPO, "profiles", "traffic.json")
         if os.path.exists(tpath):
             try:
                 tj = json.load(open(tpath))
                 if (tj.get("workload") == args.workload
-                        and tj.get("flags") == flags):
+                        and tj.get("flags") == flags
+                        and tj.get("chunks", 1) == n_chunks):
                     traffic = tj.get("hbm_bytes_per_launch")
             except (ValueError, OSError):
                 traffic = None
@@ -298,9 +366,12 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "kernel": "kl_eval_kernel",
-                "bytes_per_launch": algo_bytes,
+                "bytes_per_launch": launch_bytes,
+                "launch_ms": t_eval_launch * 1e3,
             },
-            "stages_ms": {"fit": t_fit * 1e3, "eval": t_eval * 1e3},
+            "stages_ms": {"fit": t_fit * 1e3, "eval": t_eval * 1e3,
+                          "overlap": "fit(c+1) || eval(c), %d time chunks" % n_chunks
+                          if n_chunks > 1 else "none"},
             "fit_stats": fit_stats,
             "check": {"max_abs_cos2_plus_sin2_minus_1": unit_err},
         }

@@ -91,6 +91,14 @@ int sf_create(int device, sf_ctx** out);
 int sf_destroy(sf_ctx* ctx);
 int sf_set_stream(sf_ctx* ctx, void* hip_stream); /* NULL = default stream */
 int sf_synchronize(sf_ctx* ctx);
+/* A HIP stream whose kernels may only use the compute units NOT listed in
+ * reserve_cus (CU indices 0..n_cu-1; the reserved units stay free for work
+ * on other streams, e.g. the fit of the next time chunk while the current
+ * chunk is evaluated).  n_reserve = 0 gives an ordinary stream. */
+int sf_stream_create(sf_ctx* ctx, const int* reserve_cus, int n_reserve,
+                     void** hip_stream);
+int sf_stream_destroy(sf_ctx* ctx, void* hip_stream);
+int sf_device_cus(sf_ctx* ctx, int* n_cu);
 /* Options: SF_OPT_FIT_GENERAL = 1 routes every slot through the general
  * (per-slot Jacobi) fit kernel instead of the mask-cached eigenbasis
  * pipeline; both give the reference's results (used to cross-check). */

@@ -110,6 +110,45 @@ int sf_set_stream(sf_ctx* ctx, void* stream) {
   return SF_OK;
 }
 
+int sf_device_cus(sf_ctx* ctx, int* n_cu) {
+  SF_REQUIRE(ctx && n_cu, SF_EINVAL, "sf_device_cus: NULL argument");
+  SF_HIP(hipDeviceGetAttribute(n_cu, hipDeviceAttributeMultiprocessorCount,
+                               ctx->device));
+  return SF_OK;
+}
+
+int sf_stream_create(sf_ctx* ctx, const int* reserve_cus, int n_reserve,
+                     void** stream) {
+  SF_REQUIRE(ctx && stream && n_reserve >= 0 && (n_reserve == 0 || reserve_cus),
+             SF_EINVAL, "sf_stream_create: bad argument");
+  SF_HIP(hipSetDevice(ctx->device));
+  int n_cu = 0;
+  SF_TRY(sf_device_cus(ctx, &n_cu));
+  hipStream_t s = nullptr;
+  if (n_reserve == 0) {
+    SF_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  } else {
+    std::vector<uint32_t> mask((n_cu + 31) / 32, 0u);
+    for (int c = 0; c < n_cu; ++c) mask[c >> 5] |= 1u << (c & 31);
+    for (int k = 0; k < n_reserve; ++k) {
+      const int c = reserve_cus[k];
+      SF_REQUIRE(c >= 0 && c < n_cu, SF_EINVAL, "sf_stream_create: CU index out of range");
+      mask[c >> 5] &= ~(1u << (c & 31));
+    }
+    SF_REQUIRE(n_reserve < n_cu, SF_EINVAL, "sf_stream_create: no CU left");
+    SF_HIP(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+  }
+  *stream = s;
+  return SF_OK;
+}
+
+int sf_stream_destroy(sf_ctx* ctx, void* stream) {
+  SF_REQUIRE(ctx && stream, SF_EINVAL, "sf_stream_destroy: bad argument");
+  SF_HIP(hipSetDevice(ctx->device));
+  SF_HIP(hipStreamDestroy(reinterpret_cast<hipStream_t>(stream)));
+  return SF_OK;
+}
+
 int sf_set_option(sf_ctx* ctx, int option, int value) {
   SF_REQUIRE(ctx, SF_EINVAL, "sf_set_option: NULL context");
   switch (option) {

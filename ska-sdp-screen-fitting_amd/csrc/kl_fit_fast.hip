@@ -818,7 +818,8 @@ int launch_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,
 
   static const char* env = std::getenv("SCREENFIT_FIT");
   if (ctx->force_general || (env && env[0] == 'g')) {
-    if (p->screen_type == SF_SCREEN_AMPLITUDE || p->niter > 1 && p->screen_type != SF_SCREEN_PHASE) {
+    if (p->screen_type == SF_SCREEN_AMPLITUDE ||
+        (p->niter > 1 && p->screen_type != SF_SCREEN_PHASE)) {
       set_error("the general fit kernel handles phase (any niter) and tec (niter 1) only");
       return SF_EINVAL;
     }

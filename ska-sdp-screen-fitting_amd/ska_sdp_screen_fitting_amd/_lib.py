@@ -28,6 +28,7 @@ EXPORTED = (
     "sf_version", "sf_last_error", "sf_create", "sf_destroy", "sf_set_stream",
     "sf_synchronize", "sf_set_option", "sf_alloc", "sf_free", "sf_copy_h2d", "sf_copy_d2h",
     "sf_set_basis", "sf_get_basis", "sf_kl_fit", "sf_get_fit_stats",
+    "sf_stream_create", "sf_stream_destroy", "sf_device_cus",
     "sf_set_grid", "sf_kl_eval", "sf_kl_eval_gain", "sf_tess_fill",
 )
 
@@ -82,6 +83,10 @@ def load_library(path=None):
             "sf_get_fit_stats": ([vp, ip, ip], c_int),
             "sf_set_grid": ([vp, vp, c_int, vp, c_int], c_int),
             "sf_kl_eval": ([vp, vp, i64, vp, i64, ctypes.c_uint], c_int),
+            "sf_stream_create": ([vp, ctypes.POINTER(c_int), c_int,
+                                  ctypes.POINTER(vp)], c_int),
+            "sf_stream_destroy": ([vp, vp], c_int),
+            "sf_device_cus": ([vp, ctypes.POINTER(c_int)], c_int),
             "sf_kl_eval_gain": ([vp, vp, vp, vp, i64, vp, i64, ctypes.c_uint],
                                 c_int),
             "sf_tess_fill": ([vp, vp, c_int, c_int, vp, vp, vp, c_int, i64, vp,
@@ -202,6 +207,24 @@ class Context:
         _check(self.lib.sf_kl_eval(self.h, _ptr(coef), int(S), _ptr(out),
                                    max(ring, 1), int(flags)), "sf_kl_eval")
 
+
+    def device_cus(self):
+        n = ctypes.c_int(0)
+        _check(self.lib.sf_device_cus(self.h, ctypes.byref(n)), "sf_device_cus")
+        return n.value
+
+    def stream_create(self, reserve_cus=()):
+        """Raw HIP stream (int handle) whose kernels avoid ``reserve_cus``;
+        wrap with ``torch.cuda.ExternalStream``."""
+        arr = (ctypes.c_int * max(1, len(reserve_cus)))(*reserve_cus)
+        out = ctypes.c_void_p()
+        _check(self.lib.sf_stream_create(self.h, arr, len(reserve_cus),
+                                         ctypes.byref(out)), "sf_stream_create")
+        return out.value
+
+    def stream_destroy(self, stream):
+        _check(self.lib.sf_stream_destroy(self.h, ctypes.c_void_p(stream)),
+               "sf_stream_destroy")
 
     def eval_gain(self, coef_ph, coef_xx, coef_yy, S, out, ring_slots=None,
                   flags=SF_EVAL_NAN_SCRUB | SF_EVAL_FAST_SINCOS | SF_EVAL_NT_STORES):
