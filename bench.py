@@ -227,6 +227,7 @@ def main():
     # --reserve-cus compute units (spread over the XCDs) to the fit stream, so
     # the fit of the next chunk is not starved by queued eval workgroups
     fit_stream = stream
+    masked_handle = None
     if n_chunks > 1:
         fit_stream = torch.cuda.Stream(dev, priority=-1 if args.fit_priority else 0)
         if args.reserve_cus > 0:
@@ -235,7 +236,8 @@ def main():
             # k*step + k%8: one per XCD whether CUs are numbered XCD-major
             # or interleaved across the 8 XCDs
             reserved = [min(n_cu - 1, k * step + k % 8) for k in range(args.reserve_cus)]
-            stream = torch.cuda.ExternalStream(ctx.stream_create(reserved), device=dev)
+            masked_handle = ctx.stream_create(reserved)
+            stream = torch.cuda.ExternalStream(masked_handle, device=dev)
 
     def fit(c):
         t0, t1 = bounds[c]
@@ -381,6 +383,11 @@ def main():
             line["cpu_baseline"] = cpu_baseline(
                 sol, setup, max(1, min(args.cpu_workers, os.cpu_count() or 1)))
         print(json.dumps(line), flush=True)
+    # release the CU-masked stream before the HIP runtime tears down
+    torch.cuda.synchronize(dev)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    if masked_handle is not None:
+        ctx.stream_destroy(masked_handle)
     if world > 1:
         dist.destroy_process_group()
 
