@@ -239,6 +239,8 @@ def main():
             masked_handle = ctx.stream_create(reserved)
             stream = torch.cuda.ExternalStream(masked_handle, device=dev)
 
+    eval_kernel_name = ctx.eval_kernel(flags)
+
     def fit(c):
         t0, t1 = bounds[c]
         ctx.set_stream(fit_stream.cuda_stream)
@@ -334,7 +336,8 @@ def main():
                 tj = json.load(open(tpath))
                 if (tj.get("workload") == args.workload
                         and tj.get("flags") == flags
-                        and tj.get("chunks", 1) == n_chunks):
+                        and tj.get("chunks", 1) == n_chunks
+                        and tj.get("eval_kernel") == eval_kernel_name):
                     traffic = tj.get("hbm_bytes_per_launch")
             except (ValueError, OSError):
                 traffic = None
@@ -367,7 +370,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "kl_eval_kernel",
+                "kernel": eval_kernel_name,
                 "bytes_per_launch": launch_bytes,
                 "launch_ms": t_eval_launch * 1e3,
             },

@@ -103,6 +103,21 @@ int sf_device_cus(sf_ctx* ctx, int* n_cu);
  * (per-slot Jacobi) fit kernel instead of the mask-cached eigenbasis
  * pipeline; both give the reference's results (used to cross-check). */
 #define SF_OPT_FIT_GENERAL 1
+/* SF_OPT_EVAL_KERNEL selects the evaluation kernel of sf_kl_eval (all give
+ * the same values): AUTO (default), TILE = register-tile stores (4 slots x
+ * 256 B per store instruction; always used for fp64 sincos and gain
+ * screens), LDS4 / LDS8 / LDS16 = LDS-staged stores with 1 / 2 / 4 KiB
+ * contiguous runs per (slot, plane). */
+#define SF_OPT_EVAL_KERNEL 2
+#define SF_EVAL_KERNEL_AUTO 0
+#define SF_EVAL_KERNEL_TILE 1
+#define SF_EVAL_KERNEL_LDS4 2
+#define SF_EVAL_KERNEL_LDS8 3
+#define SF_EVAL_KERNEL_LDS16 4
+/* The evaluation kernel sf_kl_eval (gain = 0) or sf_kl_eval_gain (gain = 1)
+ * runs for the current grid and these flags on a 16-byte aligned output
+ * (one of SF_EVAL_KERNEL_TILE / _LDS4 / _LDS8 / _LDS16). */
+int sf_get_eval_kernel(sf_ctx* ctx, int gain, unsigned flags, int* kernel);
 int sf_set_option(sf_ctx* ctx, int option, int value);
 int sf_alloc(sf_ctx* ctx, size_t bytes, void** dev_ptr);
 int sf_free(sf_ctx* ctx, void* dev_ptr);

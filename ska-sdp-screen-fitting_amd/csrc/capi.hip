@@ -155,10 +155,23 @@ int sf_set_option(sf_ctx* ctx, int option, int value) {
     case SF_OPT_FIT_GENERAL:
       ctx->force_general = value != 0;
       return SF_OK;
+    case SF_OPT_EVAL_KERNEL:
+      SF_REQUIRE(value >= SF_EVAL_KERNEL_AUTO && value <= SF_EVAL_KERNEL_LDS16,
+                 SF_EINVAL, "sf_set_option: unknown evaluation kernel");
+      ctx->eval_kernel = value;
+      return SF_OK;
     default:
       set_error("sf_set_option: unknown option");
       return SF_EINVAL;
   }
+}
+
+int sf_get_eval_kernel(sf_ctx* ctx, int gain, unsigned flags, int* kernel) {
+  SF_REQUIRE(ctx && kernel, SF_EINVAL, "sf_get_eval_kernel: bad argument");
+  SF_REQUIRE(ctx->ksteps > 0, SF_EINVAL,
+             "sf_get_eval_kernel: call sf_set_grid first");
+  *kernel = sf::pick_eval_kernel(ctx, gain != 0, flags, true);
+  return SF_OK;
 }
 
 int sf_synchronize(sf_ctx* ctx) {

@@ -20,6 +20,13 @@
 //     epilogue of the previous tile (independent waves on the SIMD).
 //   * block index -> (pixel block, slot chunk) is XCD-aware: the 8 XCDs each
 //     own 1/8 of the pixel blocks, so their Cpix slices stay in their L2.
+// Two store mappings share this contraction (same bits out):
+//   * kl_eval_kernel (register tile): each lane stores its own MFMA outputs,
+//     so one store instruction covers 4 slots x 256 B;
+//   * kl_eval_lds_kernel: the range-reduced phases go through LDS and each
+//     wave writes 1-4 KiB contiguous runs per (slot, plane) -- +4-7 % store
+//     bandwidth at D <= 28 (tools/eval_variants.py); the register tile stays
+//     the choice for heavier contractions, fp64 sincos and gain screens.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -216,10 +223,14 @@ __global__ __launch_bounds__(256, SF_EVAL_MIN_WAVES) void kl_eval_kernel(
       }
       float* o = out + ((s % ring) * 4) * P + p0;
       if (VEC4) {
+        // P % 4 == 0: a lane's 4 pixels are all inside the grid or all out
+        // (the last wave block of a grid that is not a multiple of 64)
+        if (p0 < P) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const v4f v = {pv[q][0], pv[q][1], pv[q][2], pv[q][3]};
-          store4<NT>(o + q * P, v);
+          for (int q = 0; q < 4; ++q) {
+            const v4f v = {pv[q][0], pv[q][1], pv[q][2], pv[q][3]};
+            store4<NT>(o + q * P, v);
+          }
         }
       } else {
 #pragma unroll
@@ -227,6 +238,139 @@ __global__ __launch_bounds__(256, SF_EVAL_MIN_WAVES) void kl_eval_kernel(
           if (p0 + t < P) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) o[q * P + t] = pv[q][t];
+          }
+        }
+      }
+    }
+  }
+}
+
+// LDS-staged variant (phase screens, fp32 sincos epilogue): the same MFMA
+// contraction, but the stores are re-mapped so that one wave writes long
+// contiguous runs.  A workgroup of NW waves covers RUN = 64*NW consecutive
+// pixels; per 16-slot group every wave drops its 16 x 64 range-reduced
+// phases (fp64 reduction to [-pi, pi], then float -- exactly the value the
+// fp32 sincos of the register-tile kernel sees) into LDS, and after one
+// barrier wave w takes slots w*16/NW.. and, per slot, sweeps the RUN pixels
+// plane by plane: RUN*4 contiguous bytes per (slot, plane) instead of 256 B.
+// The LDS tile is double-buffered, so one barrier per group suffices (a
+// wave reaches the barrier of group g only after reading group g-1).
+template <int NW>
+struct EvalLds {
+  static constexpr int kRun = 64 * NW;          // pixels per workgroup
+  static constexpr int kStride = kRun + 4;      // padded LDS row (floats)
+  static constexpr int kSlotsPerWave = 16 / NW;
+  static constexpr int kChunks = kRun / 256;    // 1-KiB store runs per plane
+};
+
+template <int KS, int NW, bool NT>
+__global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
+    const double* __restrict__ cfrag, const double* __restrict__ coef, int D,
+    int ks_real, int64_t S, int64_t P, int64_t n_pb, int64_t n_sc,
+    int chunk_groups, float* __restrict__ out, int64_t ring, unsigned flags) {
+  using L = EvalLds<NW>;
+  __shared__ float tile[2][16][L::kStride];
+  const int l = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int64_t b = blockIdx.x;
+  int64_t pb, sc;
+  if ((n_pb & 7) == 0) {
+    const int64_t per = n_pb >> 3;
+    const int64_t x = b & 7, i = b >> 3;
+    pb = x * per + (i % per);
+    sc = i / per;
+  } else {
+    pb = b % n_pb;
+    sc = b / n_pb;
+  }
+  if (sc >= n_sc) return;  // uniform per workgroup
+  const int64_t wpb = pb * NW + w;
+  const bool live = wpb * kWavePix < P;  // waves past the grid still sync
+
+  double bf[KS][kTiles];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+    for (int t = 0; t < kTiles; ++t)
+      bf[kk][t] = (live && kk < ks_real)
+                      ? cfrag[((wpb * ks_real + kk) * kTiles + t) * 64 + l]
+                      : 0.0;
+
+  const bool scrub = flags & SF_EVAL_NAN_SCRUB;
+  const bool be = flags & SF_EVAL_BIG_ENDIAN;
+  const int64_t pix0 = pb * L::kRun;
+  const int64_t slot_base = sc * (int64_t)chunk_groups * 16;
+  for (int g = 0; g < chunk_groups; ++g) {
+    const int64_t s0 = slot_base + (int64_t)g * 16;
+    if (s0 >= S) break;  // uniform per workgroup
+    float(*buf)[L::kStride] = tile[g & 1];
+    // ---- contraction: 16 slots x this wave's 64 pixels
+    double af[KS];
+    {
+      const int64_t s = s0 + (l & 15);
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) {
+        const int d = 4 * kk + (l >> 4);
+        af[kk] = (s < S && d < D) ? coef[s * D + d] : 0.0;
+      }
+    }
+    v4d acc[kTiles];
+#pragma unroll
+    for (int t = 0; t < kTiles; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+      for (int t = 0; t < kTiles; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[kk], bf[kk][t],
+                                                      acc[t], 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float red[kTiles];
+#pragma unroll
+      for (int t = 0; t < kTiles; ++t) {
+        const double ph = acc[t][r];
+        const double k = rint(ph * 0.15915494309189535);
+        double x = fma(-k, 6.283185307179586, ph);
+        x = fma(-k, 2.4492935982947064e-16, x);
+        red[t] = (float)x;
+      }
+      *reinterpret_cast<v4f*>(&buf[acc_row(l, r)][w * kWavePix + (l & 15) * kTiles]) =
+          v4f{red[0], red[1], red[2], red[3]};
+    }
+    __syncthreads();
+    // ---- stores: wave w owns kSlotsPerWave slots of the group
+#pragma unroll
+    for (int j = 0; j < L::kSlotsPerWave; ++j) {
+      const int row = w * L::kSlotsPerWave + j;
+      const int64_t s = s0 + row;
+      if (s >= S) break;
+      float cv[L::kChunks][4], sv[L::kChunks][4];
+#pragma unroll
+      for (int c = 0; c < L::kChunks; ++c) {
+        const v4f rv = *reinterpret_cast<const v4f*>(&buf[row][c * 256 + 4 * l]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float sn, cs;
+          sincosf(rv[e], &sn, &cs);
+          if (scrub && isnan(cs)) cs = 1.0f;
+          if (scrub && isnan(sn)) sn = 0.0f;
+          if (be) {
+            cs = bswapf(cs);
+            sn = bswapf(sn);
+          }
+          cv[c][e] = cs;
+          sv[c][e] = sn;
+        }
+      }
+      float* o = out + ((s % ring) * 4) * P + pix0 + 4 * l;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int c = 0; c < L::kChunks; ++c) {
+          if (pix0 + c * 256 + 4 * l < P) {
+            const v4f v = (q & 1) ? v4f{sv[c][0], sv[c][1], sv[c][2], sv[c][3]}
+                                  : v4f{cv[c][0], cv[c][1], cv[c][2], cv[c][3]};
+            store4<NT>(o + q * P + c * 256, v);
           }
         }
       }
@@ -289,13 +433,74 @@ static int launch_eval_ks(sf_ctx* ctx, const double* coef,
   return SF_OK;
 }
 
+template <int KS, int NW>
+static int launch_eval_lds(sf_ctx* ctx, const double* coef, int64_t S,
+                           float* out, int64_t ring, unsigned flags) {
+  const int64_t P = ctx->n_pix;
+  const int64_t run = EvalLds<NW>::kRun;
+  const int64_t n_pb = (P + run - 1) / run;
+  int groups = 16;
+  while (groups > 1 && n_pb * ((S + 16 * groups - 1) / (16 * groups)) < 1024)
+    groups >>= 1;
+  const int64_t n_sc = (S + 16 * groups - 1) / (16 * groups);
+  int64_t nblk = n_pb * n_sc;
+  if ((n_pb & 7) == 0) nblk = ((nblk + 7) / 8) * 8;
+  if (flags & SF_EVAL_NT_STORES)
+    hipLaunchKernelGGL((kl_eval_lds_kernel<KS, NW, true>), dim3((unsigned)nblk),
+                       dim3(64 * NW), 0, ctx->stream, ctx->d_cfrag, coef, ctx->D,
+                       ctx->ksteps, S, P, n_pb, n_sc, groups, out, ring, flags);
+  else
+    hipLaunchKernelGGL((kl_eval_lds_kernel<KS, NW, false>), dim3((unsigned)nblk),
+                       dim3(64 * NW), 0, ctx->stream, ctx->d_cfrag, coef, ctx->D,
+                       ctx->ksteps, S, P, n_pb, n_sc, groups, out, ring, flags);
+  SF_HIP(hipGetLastError());
+  return SF_OK;
+}
+
+// Kernel sf_kl_eval runs for this context, output alignment and flags.
+int pick_eval_kernel(const sf_ctx* ctx, bool gain, unsigned flags,
+                     bool out_aligned16) {
+  // the LDS-staged kernel covers phase screens with the fp32 sincos
+  // epilogue and float4-aligned output; everything else (fp64 sincos, gain
+  // screens, odd grids) takes the register-tile kernel
+  const bool lds_ok = !gain && (flags & SF_EVAL_FAST_SINCOS) &&
+                      (ctx->n_pix % 4 == 0) && out_aligned16;
+  if (!lds_ok) return SF_EVAL_KERNEL_TILE;
+  if (ctx->eval_kernel != SF_EVAL_KERNEL_AUTO) return ctx->eval_kernel;
+  // measured on MI355X (tools/eval_variants.py, profiles/round1d_eval_variants.txt):
+  // long store runs win while the contraction is light; from ksteps 8 on
+  // (D > 28) the per-group barrier serialises MFMA and stores and the
+  // register-tile kernel is faster
+  if (ctx->ksteps <= 2) return SF_EVAL_KERNEL_LDS4;
+  if (ctx->ksteps <= 7) return SF_EVAL_KERNEL_LDS16;
+  return SF_EVAL_KERNEL_TILE;
+}
+
+template <int KS>
+static int launch_eval_pick(sf_ctx* ctx, const double* coef, const double* cxx,
+                            const double* cyy, int64_t S, float* out,
+                            int64_t ring, unsigned flags) {
+  const int v = pick_eval_kernel(ctx, cxx != nullptr, flags,
+                                 (reinterpret_cast<uintptr_t>(out) & 15) == 0);
+  switch (v) {
+    case SF_EVAL_KERNEL_LDS4:
+      return launch_eval_lds<KS, 4>(ctx, coef, S, out, ring, flags);
+    case SF_EVAL_KERNEL_LDS8:
+      return launch_eval_lds<KS, 8>(ctx, coef, S, out, ring, flags);
+    case SF_EVAL_KERNEL_LDS16:
+      return launch_eval_lds<KS, 16>(ctx, coef, S, out, ring, flags);
+    default:
+      return launch_eval_ks<KS>(ctx, coef, cxx, cyy, S, out, ring, flags);
+  }
+}
+
 int launch_eval(sf_ctx* ctx, const double* coef, const double* cxx,
                 const double* cyy, int64_t S, float* out, int64_t ring,
                 unsigned flags) {
   switch (ctx->ksteps) {
 #define SF_KS(k) \
   case k:        \
-    return launch_eval_ks<k>(ctx, coef, cxx, cyy, S, out, ring, flags);
+    return launch_eval_pick<k>(ctx, coef, cxx, cyy, S, out, ring, flags);
     SF_KS(1) SF_KS(2) SF_KS(3) SF_KS(4) SF_KS(5) SF_KS(6) SF_KS(7) SF_KS(8)
     SF_KS(9) SF_KS(10) SF_KS(11) SF_KS(12) SF_KS(13) SF_KS(14) SF_KS(15)
 #undef SF_KS

@@ -83,6 +83,8 @@ struct sf_ctx {
   double* d_gw = nullptr;
   // fast-path switch (SCREENFIT_FIT=general forces the general kernel)
   int force_general = 0;
+  // evaluation kernel (SF_OPT_EVAL_KERNEL)
+  int eval_kernel = SF_EVAL_KERNEL_AUTO;
 };
 
 namespace sf {
@@ -104,6 +106,8 @@ int launch_cpix(sf_ctx* ctx, const double* d_x, const double* d_y);
 int launch_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,
                int F, int A, const sf_fit_params* p, double* coef,
                double* resid, float* w_out, int32_t* order_out);
+int pick_eval_kernel(const sf_ctx* ctx, bool gain, unsigned flags,
+                     bool out_aligned16);
 int launch_eval(sf_ctx* ctx, const double* coef, const double* cxx,
                 const double* cyy, int64_t S, float* out, int64_t ring,
                 unsigned flags);

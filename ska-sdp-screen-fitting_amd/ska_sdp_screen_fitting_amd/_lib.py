@@ -22,11 +22,21 @@ SF_EVAL_NT_STORES = 1 << 9
 SF_EVAL_BIG_ENDIAN = 1 << 10
 SF_MAX_DIR = 60
 SF_OPT_FIT_GENERAL = 1
+SF_OPT_EVAL_KERNEL = 2
+SF_EVAL_KERNEL_AUTO = 0
+SF_EVAL_KERNEL_TILE = 1
+SF_EVAL_KERNEL_LDS4 = 2
+SF_EVAL_KERNEL_LDS8 = 3
+SF_EVAL_KERNEL_LDS16 = 4
+EVAL_KERNEL_NAMES = {SF_EVAL_KERNEL_TILE: "kl_eval_kernel",
+                     SF_EVAL_KERNEL_LDS4: "kl_eval_lds_kernel<4 waves>",
+                     SF_EVAL_KERNEL_LDS8: "kl_eval_lds_kernel<8 waves>",
+                     SF_EVAL_KERNEL_LDS16: "kl_eval_lds_kernel<16 waves>"}
 
 # every symbol include/screenfit.h declares (checked by tests/test_capi.py)
 EXPORTED = (
     "sf_version", "sf_last_error", "sf_create", "sf_destroy", "sf_set_stream",
-    "sf_synchronize", "sf_set_option", "sf_alloc", "sf_free", "sf_copy_h2d", "sf_copy_d2h",
+    "sf_synchronize", "sf_set_option", "sf_get_eval_kernel", "sf_alloc", "sf_free", "sf_copy_h2d", "sf_copy_d2h",
     "sf_set_basis", "sf_get_basis", "sf_kl_fit", "sf_get_fit_stats",
     "sf_stream_create", "sf_stream_destroy", "sf_device_cus",
     "sf_set_grid", "sf_kl_eval", "sf_kl_eval_gain", "sf_tess_fill",
@@ -72,6 +82,7 @@ def load_library(path=None):
             "sf_set_stream": ([vp, vp], c_int),
             "sf_synchronize": ([vp], c_int),
             "sf_set_option": ([vp, c_int, c_int], c_int),
+            "sf_get_eval_kernel": ([vp, c_int, ctypes.c_uint, ip], c_int),
             "sf_alloc": ([vp, ctypes.c_size_t, ctypes.POINTER(vp)], c_int),
             "sf_free": ([vp, vp], c_int),
             "sf_copy_h2d": ([vp, vp, vp, ctypes.c_size_t], c_int),
@@ -151,6 +162,13 @@ class Context:
     def set_option(self, option, value):
         _check(self.lib.sf_set_option(self.h, int(option), int(value)),
                "sf_set_option")
+
+    def eval_kernel(self, flags, gain=False):
+        """Name of the evaluation kernel sf_kl_eval runs for these flags."""
+        k = ctypes.c_int()
+        _check(self.lib.sf_get_eval_kernel(self.h, int(bool(gain)), int(flags),
+                                           ctypes.byref(k)), "sf_get_eval_kernel")
+        return EVAL_KERNEL_NAMES[k.value]
 
     def synchronize(self):
         _check(self.lib.sf_synchronize(self.h), "sf_synchronize")

@@ -287,3 +287,46 @@ def test_make_aterm_image_from_h5parm_file(tmp_path):
                          padding_fraction=0, cellsize_deg=0.2, ncpu=0)
         cubes.append(sffits.read_cube(outroot + "_0.fits")[1])
     np.testing.assert_array_equal(cubes[0], cubes[1])
+
+
+@pytest.mark.parametrize("n_dir,grid", [(20, 256), (7, 128), (24, 60), (50, 64), (3, 40)])
+def test_eval_kernels_agree(ctx, dev, n_dir, grid):
+    """Every evaluation kernel (register-tile, LDS-staged 1/2/4 KiB runs;
+    plain and non-temporal stores; big-endian) writes the same bits, and the
+    fp32-sincos result is within 2e-6 of the oracle.  Ragged slot count,
+    grids that are not a multiple of the store run, a NaN slot."""
+    from ska_sdp_screen_fitting_amd import geometry
+    from ska_sdp_screen_fitting_amd._lib import (
+        SF_EVAL_BIG_ENDIAN, SF_EVAL_FAST_SINCOS, SF_EVAL_KERNEL_AUTO,
+        SF_EVAL_KERNEL_LDS4, SF_EVAL_KERNEL_LDS8, SF_EVAL_KERNEL_LDS16,
+        SF_EVAL_KERNEL_TILE, SF_EVAL_NT_STORES, SF_OPT_EVAL_KERNEL)
+    from ska_sdp_screen_fitting_amd.synthetic import make_solutions
+    s = make_solutions(n_ant=2, n_time=2, n_freq=1, n_dir=n_dir, seed=4)
+    pp, mra, mdec = geometry.piercepoints(s.dir_radec)
+    cell = FIELD["width"] / (grid - 0.5)
+    x, y = geometry.grid_coords(FIELD["rad"], FIELD["dec"], FIELD["width"],
+                                cell, mra, mdec)
+    rng = np.random.default_rng(n_dir + grid)
+    coef = rng.normal(0, 0.01, size=(45, n_dir))
+    coef[9, n_dir // 2] = np.nan
+    base = 1 | SF_EVAL_FAST_SINCOS
+    outs = {}
+    try:
+        for kv in (SF_EVAL_KERNEL_TILE, SF_EVAL_KERNEL_LDS4, SF_EVAL_KERNEL_LDS8,
+                   SF_EVAL_KERNEL_LDS16, SF_EVAL_KERNEL_AUTO):
+            ctx.set_option(SF_OPT_EVAL_KERNEL, kv)
+            for extra in (0, SF_EVAL_NT_STORES, SF_EVAL_BIG_ENDIAN):
+                o = gpu_eval(ctx, dev, pp, x, y, coef, flags=base | extra)
+                if extra == SF_EVAL_BIG_ENDIAN:
+                    o = o.byteswap()
+                outs[(kv, extra)] = o
+    finally:
+        ctx.set_option(SF_OPT_EVAL_KERNEL, SF_EVAL_KERNEL_AUTO)
+    ref = outs[(SF_EVAL_KERNEL_TILE, 0)]
+    for k, o in outs.items():
+        assert np.array_equal(o.view(np.int32), ref.view(np.int32)), k
+    assert np.all(ref[9, 0] == 1.0) and np.all(ref[9, 1] == 0.0)
+    cpix = okl.cpix_matrix(pp, x, y)
+    good = np.isfinite(coef).all(axis=1)
+    want = okl.eval_planes(okl.eval_phase_screens(coef[good], cpix))
+    np.testing.assert_allclose(ref[good].reshape(want.shape), want, rtol=0, atol=2e-6)

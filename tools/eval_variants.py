@@ -1,44 +1,106 @@
-"""Repeated, interleaved timing of eval variants (plain vs non-temporal)."""
+"""Interleaved timing of the evaluation kernels (sf_kl_eval variants) on one
+GPU, plus a bitwise cross-check of their outputs.
+
+    python tools/eval_variants.py [--variants tile+nt,lds16+nt] D:N [D:N ...]
+
+Every repetition runs every (shape, variant) pair once, so box-to-box and
+drift effects hit all of them alike.
+"""
+import argparse
 import os
 import sys
-import time
 
 import numpy as np
 import torch
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "ska-sdp-screen-fitting_amd"))
-from ska_sdp_screen_fitting_amd import geometry, get_context  # noqa: E402
-from ska_sdp_screen_fitting_amd._lib import (SF_EVAL_FAST_SINCOS,  # noqa: E402
-                                             SF_EVAL_NT_STORES)
+from ska_sdp_screen_fitting_amd import get_context  # noqa: E402
+from ska_sdp_screen_fitting_amd._lib import (  # noqa: E402
+    SF_EVAL_FAST_SINCOS, SF_EVAL_KERNEL_AUTO, SF_EVAL_KERNEL_LDS4,
+    SF_EVAL_KERNEL_LDS8, SF_EVAL_KERNEL_LDS16, SF_EVAL_KERNEL_TILE,
+    SF_EVAL_NAN_SCRUB, SF_EVAL_NT_STORES, SF_OPT_EVAL_KERNEL)
+
+KERNELS = {"auto": SF_EVAL_KERNEL_AUTO, "tile": SF_EVAL_KERNEL_TILE,
+           "lds4": SF_EVAL_KERNEL_LDS4, "lds8": SF_EVAL_KERNEL_LDS8,
+           "lds16": SF_EVAL_KERNEL_LDS16}
+
+ap = argparse.ArgumentParser()
+ap.add_argument("shapes", nargs="*", default=["20:256"])
+ap.add_argument("--variants", default=",".join(
+    f"{k}{s}" for k in KERNELS if k != "auto" for s in ("", "+nt")))
+ap.add_argument("--reps", type=int, default=7)
+ap.add_argument("--slots", type=int, default=102400,
+                help="slots per launch at 256^2 (scaled by 256^2/N^2)")
+args = ap.parse_args()
 
 dev = torch.device("cuda", 0)
 ctx = get_context(0)
 stream = torch.cuda.current_stream(dev)
 ctx.set_stream(stream.cuda_stream)
-rng = np.random.default_rng(0)
-D, N = int(sys.argv[1]) if len(sys.argv) > 1 else 20, 256
-S = 102400
-pp = np.stack([rng.uniform(-3000, 3000, D), rng.uniform(-3000, 3000, D), np.zeros(D)], 1)
-ctx.set_basis(pp)
-x = np.linspace(-2000, 2000, N)
-ctx.set_grid(x, x)
-coef = torch.from_numpy(rng.normal(0, 0.01, (S, D))).to(dev)
-ring = 16384
-out = torch.empty((ring, 4, N, N), dtype=torch.float32, device=dev)
-variants = {"fast": 1 | SF_EVAL_FAST_SINCOS,
-            "fast+nt": 1 | SF_EVAL_FAST_SINCOS | SF_EVAL_NT_STORES}
-res = {k: [] for k in variants}
-for rep in range(6):
-    for k, fl in variants.items():
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        ctx.eval(coef, S, out, ring, fl)
-        e1.record(stream)
+base = SF_EVAL_NAN_SCRUB | SF_EVAL_FAST_SINCOS
+variants = {}
+for v in args.variants.split(","):
+    k, _, nt = v.partition("+")
+    variants[v] = (KERNELS[k], base | (SF_EVAL_NT_STORES if nt == "nt" else 0))
+
+ring_bytes = 16 * 2 ** 30
+out_flat = torch.empty(ring_bytes // 4, dtype=torch.float32, device=dev)
+shapes = []
+for sh in args.shapes:
+    D, N = (int(x) for x in sh.split(":"))
+    rng = np.random.default_rng(D * 1000 + N)
+    pp = np.stack([rng.uniform(-3000, 3000, D), rng.uniform(-3000, 3000, D),
+                   np.zeros(D)], 1)
+    S = args.slots * (256 * 256) // (N * N)
+    coef = torch.from_numpy(rng.normal(0, 0.01, (S, D))).to(dev)
+    shapes.append((D, N, S, pp, coef))
+
+
+def select(D, N, pp):
+    ctx.set_basis(pp)
+    x = np.linspace(-2000, 2000, N)
+    ctx.set_grid(x, x)
+
+
+# bitwise cross-check on a small ragged batch with a NaN coefficient
+for D, N, S, pp, coef in shapes:
+    select(D, N, pp)
+    Sc = 37
+    cchk = coef[:Sc].clone()
+    cchk[5, min(3, D - 1)] = float("nan")
+    ref = None
+    for name, (kv, fl) in variants.items():
+        ctx.set_option(SF_OPT_EVAL_KERNEL, kv)
+        o = torch.full((Sc, 4, N, N), -7.0, dtype=torch.float32, device=dev)
+        ctx.eval(cchk, Sc, o, Sc, fl)
         torch.cuda.synchronize()
-        if rep:
-            res[k].append(e0.elapsed_time(e1))
-for k, v in res.items():
+        if ref is None:
+            ref, rname = o, name
+        elif not torch.equal(o.view(torch.int32), ref.view(torch.int32)):
+            print(f"check D={D} N={N} {name}: DIFFERENT from {rname} "
+                  f"(max |d| {float((o - ref).abs().max()):.3g})", flush=True)
+            sys.exit(1)
+    print(f"check D={D} N={N}: all variants bitwise equal", flush=True)
+
+res = {}
+for rep in range(args.reps):
+    for D, N, S, pp, coef in shapes:
+        select(D, N, pp)
+        ring = ring_bytes // (16 * N * N)
+        out = out_flat[: ring * 4 * N * N].view(ring, 4, N, N)
+        for name, (kv, fl) in variants.items():
+            ctx.set_option(SF_OPT_EVAL_KERNEL, kv)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            ctx.eval(coef, S, out, ring, fl)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            if rep:
+                res.setdefault((D, N, S, name), []).append(e0.elapsed_time(e1))
+for (D, N, S, name), v in res.items():
     ms = float(np.median(v))
-    print(f"D={D} {k:8s}: median {ms:.2f} ms  min {min(v):.2f}  "
-          f"{S * (16 * N * N + 8 * D) / ms / 1e6:.1f} GB/s", flush=True)
+    gbs = S * (16 * N * N + 8 * D) / ms / 1e6
+    print(f"D={D:2d} N={N} {name:10s}: median {ms:.3f} ms  min {min(v):.3f}  "
+          f"{gbs:.1f} GB/s  frac {gbs / 8000:.3f}", flush=True)

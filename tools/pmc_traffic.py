@@ -6,7 +6,8 @@ profiles/traffic.json, which bench.py reads when workload / flags / chunks
 match its own run.
 
   python tools/pmc_traffic.py WRITE.csv FETCH.csv --workload config3 \
-      --flags 769 --chunks 4 --slots 25600 --grid 256 --n-dir 20
+      --flags 769 --chunks 2 --slots 51200 --grid 256 --n-dir 20 \
+      --eval-kernel 'kl_eval_lds_kernel<16 waves>'
 """
 import argparse
 import csv
@@ -16,7 +17,7 @@ import os
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def per_launch(path, counter, kernel="kl_eval_kernel"):
+def per_launch(path, counter, kernel="sf::kl_eval"):
     vals, name = [], None
     for r in csv.DictReader(open(path)):
         if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
@@ -37,6 +38,8 @@ def main():
     ap.add_argument("--slots", type=int, required=True, help="slots per launch")
     ap.add_argument("--grid", type=int, required=True)
     ap.add_argument("--n-dir", type=int, required=True)
+    ap.add_argument("--eval-kernel", required=True,
+                    help="bench.py's roofline.kernel for the profiled run")
     ap.add_argument("--out", default=os.path.join(REPO, "profiles", "traffic.json"))
     a = ap.parse_args()
     w_kb, nw, name = per_launch(a.write_csv, "WRITE_SIZE")
@@ -44,7 +47,8 @@ def main():
     wb, fb = w_kb * 1024.0, 2.0 * f_kb * 1024.0
     algo = a.slots * (16 * a.grid * a.grid + 8 * a.n_dir)
     out = {
-        "workload": a.workload, "kernel": name, "flags": a.flags,
+        "workload": a.workload, "kernel": name, "eval_kernel": a.eval_kernel,
+        "flags": a.flags,
         "chunks": a.chunks, "launches_averaged": min(nw, nf),
         "write_bytes": wb, "fetch_bytes_corrected_x2": fb,
         "hbm_bytes_per_launch": wb + fb,

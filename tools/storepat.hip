@@ -1,20 +1,30 @@
-// Store-pattern probe: the eval kernel's exact output address pattern with no
-// compute, versus longer contiguous runs, to see what the pattern alone can
-// reach.  out[S][4][P] float32, P = 256^2, 16 GiB.
-//   A: eval mapping -- wave = 64 px x 16 slots; one float4 store instruction
-//      covers 4 slots x 256 B (per plane)
-//   B: wave = 256 px x 4 slots; one instruction covers 1 slot x 1 KiB
-//   C: grid-stride fill (upper bound)
+// Store-pattern probe: the eval kernel's output address pattern with no
+// compute, versus longer contiguous runs, to see what each candidate mapping
+// can reach.  out[S][4][P] float32, P = 256^2, S = 16384 -> 16 GiB.
+//   A: current eval mapping -- wave = 64 px x 16 slots; one float4 store
+//      instruction covers 4 slots x 256 B (per plane)
+//   B: workgroup = 256 px x 16 slots, wave = 4 slots (LDS transpose);
+//      one instruction covers 1 slot x 1 KiB
+//   D: workgroup = 1024 px x 16 slots: 4 KiB contiguous per (slot, plane)
+//   H: workgroup = 4 slots x all P pixels: each wave writes its slot's 1 MiB
+//      (4 planes) front to back
+//   W: workgroup = 16 slots x 4096 px stripe: 16 KiB per (slot, plane)
+//   C: grid-stride fill (upper bound), grid 4096 / 16384 / 65536
+//   E: each wave owns one contiguous chunk and streams through it
+// Every pattern in a non-temporal and a plain-store flavour.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
 typedef float v4f __attribute__((ext_vector_type(4)));
+template <bool NT>
 __device__ __forceinline__ void st(float* p, v4f v) {
-  __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(p));
+  if (NT) __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(p));
+  else *reinterpret_cast<v4f*>(p) = v;
 }
 
 constexpr long P = 65536;
 
+template <bool NT>
 __global__ __launch_bounds__(256) void patA(float* out, long S, long n_pb) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const long b = blockIdx.x;
@@ -30,39 +40,19 @@ __global__ __launch_bounds__(256) void patA(float* out, long S, long n_pb) {
       float* o = out + s * 4 * P + p0;
       v4f v = {1.f, 2.f, 3.f, (float)r};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) st(o + q * P, v);
+      for (int q = 0; q < 4; ++q) st<NT>(o + q * P, v);
     }
   }
 }
 
-__global__ __launch_bounds__(256) void patB(float* out, long S, long n_pb) {
+// run = contiguous pixels per (slot, plane) owned by one workgroup
+template <bool NT, int RUN>
+__global__ __launch_bounds__(256) void patRun(float* out, long S, long n_pb) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const long b = blockIdx.x;
   const long per = n_pb >> 3, x = b & 7, i = b >> 3;
   const long pb = x * per + (i % per), sc = i / per;
-  const long p0 = pb * 256 + l * 4;
-  for (int g = 0; g < 16; ++g) {
-    const long s0 = sc * 256 + g * 16;
-    if (s0 >= S) break;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const long s = s0 + w * 4 + r;
-      float* o = out + s * 4 * P + p0;
-      v4f v = {1.f, 2.f, 3.f, (float)r};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) st(o + q * P, v);
-    }
-  }
-}
-
-// D: wave = 1024 px x 1 slot per group row: 4 consecutive 1 KiB stores per
-// (slot, plane) -> 4 KiB contiguous per wave
-__global__ __launch_bounds__(256) void patD(float* out, long S, long n_pb4) {
-  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const long b = blockIdx.x;
-  const long per = n_pb4 >> 3, x = b & 7, i = b >> 3;
-  const long pb = x * per + (i % per), sc = i / per;
-  const long p0 = pb * 1024 + l * 4;
+  const long p0 = pb * RUN + l * 4;
   for (int g = 0; g < 16; ++g) {
     const long s0 = sc * 256 + g * 16;
     if (s0 >= S) break;
@@ -74,12 +64,22 @@ __global__ __launch_bounds__(256) void patD(float* out, long S, long n_pb4) {
 #pragma unroll
       for (int q = 0; q < 4; ++q)
 #pragma unroll
-        for (int h = 0; h < 4; ++h) st(o + q * P + h * 256, v);
+        for (int h = 0; h < RUN / 256; ++h) st<NT>(o + q * P + h * 256, v);
     }
   }
 }
 
-// E: each wave owns a contiguous chunk and streams through it
+template <bool NT>
+__global__ __launch_bounds__(256) void patH(float* out, long S) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long s = (long)blockIdx.x * 4 + w;
+  if (s >= S) return;
+  float* o = out + s * 4 * P;
+  v4f v = {1.f, 2.f, 3.f, 4.f};
+  for (long i = 0; i < 4 * P; i += 256) st<NT>(o + i + l * 4, v);
+}
+
+template <bool NT>
 __global__ __launch_bounds__(256) void patE(float* out, long n4, long per_wave) {
   const int l = threadIdx.x & 63;
   const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -88,16 +88,42 @@ __global__ __launch_bounds__(256) void patE(float* out, long n4, long per_wave) 
     const long k = base + i + l;
     if (k < n4) {
       v4f v = {1.f, 2.f, 3.f, 4.f};
-      st(out + 4 * k, v);
+      st<NT>(out + 4 * k, v);
     }
   }
 }
 
+template <bool NT>
 __global__ __launch_bounds__(256) void patC(float* out, long n4) {
   const long stride = (long)gridDim.x * blockDim.x;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     v4f v = {1.f, 2.f, 3.f, 4.f};
-    st(out + 4 * i, v);
+    st<NT>(out + 4 * i, v);
+  }
+}
+
+template <bool NT>
+static void launch(int k, float* out, long S, size_t bytes) {
+  const long n_pb = P / 256, n_sc = S / 256, n4 = (long)(bytes / 16);
+  switch (k) {
+    case 0: hipLaunchKernelGGL(patA<NT>, dim3(n_pb * n_sc), dim3(256), 0, 0, out, S, n_pb); break;
+    case 1: hipLaunchKernelGGL((patRun<NT, 256>), dim3(n_pb * n_sc), dim3(256), 0, 0, out, S, n_pb); break;
+    case 2: hipLaunchKernelGGL((patRun<NT, 1024>), dim3(n_pb / 4 * n_sc), dim3(256), 0, 0, out, S, n_pb / 4); break;
+    case 3: hipLaunchKernelGGL((patRun<NT, 4096>), dim3(n_pb / 16 * n_sc), dim3(256), 0, 0, out, S, n_pb / 16); break;
+    case 4: hipLaunchKernelGGL(patH<NT>, dim3(S / 4), dim3(256), 0, 0, out, S); break;
+    case 5: hipLaunchKernelGGL(patC<NT>, dim3(4096), dim3(256), 0, 0, out, n4); break;
+    case 6: hipLaunchKernelGGL(patC<NT>, dim3(16384), dim3(256), 0, 0, out, n4); break;
+    case 7: hipLaunchKernelGGL(patC<NT>, dim3(65536), dim3(256), 0, 0, out, n4); break;
+    case 8: {
+      const long waves = 16384L * 4;
+      hipLaunchKernelGGL(patE<NT>, dim3(16384), dim3(256), 0, 0, out, n4, (n4 + waves - 1) / waves);
+      break;
+    }
+    case 9: {
+      const long waves = 2048L * 4;
+      hipLaunchKernelGGL(patE<NT>, dim3(2048), dim3(256), 0, 0, out, n4, (n4 + waves - 1) / waves);
+      break;
+    }
   }
 }
 
@@ -106,29 +132,38 @@ int main() {
   const size_t bytes = (size_t)S * 4 * P * 4;
   float* out;
   if (hipMalloc(&out, bytes) != hipSuccess) return 1;
-  const long n_pb = P / 256, n_sc = S / 256;
+  const char* names[] = {"A  eval 4slot x 256B", "B  1 KiB runs (LDS transpose)",
+                         "D  4 KiB runs", "W  16 KiB runs", "H  slot-sequential 1 MiB/wave",
+                         "C  grid-stride 4096", "C  grid-stride 16384", "C  grid-stride 65536",
+                         "E  wave chunks 16384 wg", "E  wave chunks 2048 wg"};
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  for (int k = 0; k < 5; ++k) {
-    float best = 1e9;
-    for (int rep = 0; rep < 5; ++rep) {
-      hipEventRecord(e0);
-      if (k == 0) hipLaunchKernelGGL(patA, dim3(n_pb * n_sc), dim3(256), 0, 0, out, S, n_pb);
-      if (k == 1) hipLaunchKernelGGL(patB, dim3(n_pb * n_sc), dim3(256), 0, 0, out, S, n_pb);
-      if (k == 2) hipLaunchKernelGGL(patC, dim3(16384), dim3(256), 0, 0, out, (long)(bytes / 16));
-      if (k == 3) hipLaunchKernelGGL(patD, dim3(n_pb / 4 * n_sc), dim3(256), 0, 0, out, S, n_pb / 4);
-      if (k == 4) {
-        const long n4 = (long)(bytes / 16), waves = 16384L * 4;
-        hipLaunchKernelGGL(patE, dim3(16384), dim3(256), 0, 0, out, n4, (n4 + waves - 1) / waves);
+  for (int nt = 1; nt >= 0; --nt) {
+    for (int k = 0; k < 10; ++k) {
+      float best = 1e9;
+      for (int rep = 0; rep < 5; ++rep) {
+        hipEventRecord(e0);
+        if (nt) launch<true>(k, out, S, bytes); else launch<false>(k, out, S, bytes);
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        if (rep && ms < best) best = ms;
       }
-      hipEventRecord(e1);
-      hipEventSynchronize(e1);
-      float ms;
-      hipEventElapsedTime(&ms, e0, e1);
-      if (rep && ms < best) best = ms;
+      printf("nt=%d %-32s %.1f GB/s (%.3f ms)\n", nt, names[k], bytes / (best * 1e-3) / 1e9, best);
     }
-    printf("pattern %c: %.1f GB/s (%.3f ms)\n", "ABCDE"[k], bytes / (best * 1e-3) / 1e9, best);
   }
+  float best = 1e9;
+  for (int rep = 0; rep < 5; ++rep) {
+    hipEventRecord(e0);
+    hipMemsetAsync(out, 0, bytes, 0);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms;
+    hipEventElapsedTime(&ms, e0, e1);
+    if (rep && ms < best) best = ms;
+  }
+  printf("hipMemset %.1f GB/s (%.3f ms)\n", bytes / (best * 1e-3) / 1e9, best);
   return 0;
 }
