@@ -37,9 +37,6 @@ namespace sf {
 
 typedef double v4d __attribute__((ext_vector_type(4)));
 
-#ifndef SF_EVAL_MIN_WAVES
-#define SF_EVAL_MIN_WAVES 2
-#endif
 
 
 // f64 16x16x4 accumulator layout on gfx950: lane l, register r holds
@@ -80,6 +77,28 @@ __global__ __launch_bounds__(256) void kl_cpix_kernel(
   cfrag[e] = v;
 }
 
+// sin / cos of a phase already reduced to [-pi, pi] (in fp64, then rounded
+// to float): quadrant split with a two-part pi/2 and Cephes' single-precision
+// minimax polynomials on [-pi/4, pi/4] -- branch-free, ~20 VALU ops, error
+// <= 2e-7 beyond the float rounding of the argument.  NaN in, NaN out.
+__device__ __forceinline__ void sincos_reduced(float r, float& s, float& c) {
+  const float q = rintf(r * 0.63661977236758134f);
+  float y = fmaf(-q, 1.5707963705062866f, r);
+  y = fmaf(-q, -4.3711390001862412e-08f, y);
+  const float z = y * y;
+  float ps = fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f);
+  ps = fmaf(z, ps, -1.6666654611e-1f);
+  ps = fmaf(y * z, ps, y);
+  float pc = fmaf(z, 2.443315711809948e-5f, -1.388731625493765e-3f);
+  pc = fmaf(z, pc, 4.166664568298827e-2f);
+  pc = fmaf(z * z, pc, fmaf(-0.5f, z, 1.0f));
+  const int iq = (int)q;
+  const float a = (iq & 1) ? pc : ps;
+  const float b = (iq & 1) ? ps : pc;
+  s = (iq & 2) ? -a : a;
+  c = ((iq + 1) & 2) ? -b : b;
+}
+
 template <bool FAST>
 __device__ __forceinline__ void jones_sincos(double ph, float& s, float& c) {
   if (FAST) {
@@ -87,7 +106,7 @@ __device__ __forceinline__ void jones_sincos(double ph, float& s, float& c) {
     const double k = rint(ph * 0.15915494309189535);
     double r = fma(-k, 6.283185307179586, ph);
     r = fma(-k, 2.4492935982947064e-16, r);
-    sincosf((float)r, &s, &c);
+    sincos_reduced((float)r, s, c);
   } else {
     double sd, cd;
     sincos(ph, &sd, &cd);
@@ -97,6 +116,7 @@ __device__ __forceinline__ void jones_sincos(double ph, float& s, float& c) {
 }
 
 typedef float v4f __attribute__((ext_vector_type(4)));
+typedef float v2f __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ float bswapf(float x) {
   return __uint_as_float(__builtin_bswap32(__float_as_uint(x)));
@@ -115,8 +135,8 @@ __device__ __forceinline__ double amp10(double x) {
   return exp10(x);
 }
 
-template <int KS, bool VEC4, bool FAST, bool NT, bool GAIN>
-__global__ __launch_bounds__(256, SF_EVAL_MIN_WAVES) void kl_eval_kernel(
+template <int KS, int MINW, bool VEC4, bool FAST, bool NT, bool GAIN>
+__global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
     const double* __restrict__ cfrag, const double* __restrict__ coef,
     const double* __restrict__ coef_xx, const double* __restrict__ coef_yy,
     int D, int64_t S, int64_t P, int64_t n_pb, int64_t n_sc, int chunk_groups,
@@ -255,20 +275,25 @@ __global__ __launch_bounds__(256, SF_EVAL_MIN_WAVES) void kl_eval_kernel(
 // plane by plane: RUN*4 contiguous bytes per (slot, plane) instead of 256 B.
 // The LDS tile is double-buffered, so one barrier per group suffices (a
 // wave reaches the barrier of group g only after reading group g-1).
-template <int NW>
+// TPW = MFMA tiles per wave: 4 (the wave owns a whole 64-pixel block, as in
+// the register-tile kernel) or 2 (two waves share a block, each holding half
+// of its Cpix fragments -- half the registers, for large D).
+template <int NW, int TPW>
 struct EvalLds {
-  static constexpr int kRun = 64 * NW;          // pixels per workgroup
+  static constexpr int kWavesPerBlock = kTiles / TPW;
+  static constexpr int kRun = kWavePix * NW / kWavesPerBlock;  // pixels per workgroup
   static constexpr int kStride = kRun + 4;      // padded LDS row (floats)
   static constexpr int kSlotsPerWave = 16 / NW;
   static constexpr int kChunks = kRun / 256;    // 1-KiB store runs per plane
+  static_assert(kRun % 256 == 0 && 16 % NW == 0, "bad LDS eval shape");
 };
 
-template <int KS, int NW, bool NT>
+template <int KS, int NW, int TPW, bool NT>
 __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
     const double* __restrict__ cfrag, const double* __restrict__ coef, int D,
     int ks_real, int64_t S, int64_t P, int64_t n_pb, int64_t n_sc,
     int chunk_groups, float* __restrict__ out, int64_t ring, unsigned flags) {
-  using L = EvalLds<NW>;
+  using L = EvalLds<NW, TPW>;
   __shared__ float tile[2][16][L::kStride];
   const int l = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
@@ -284,16 +309,18 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
     sc = b / n_pb;
   }
   if (sc >= n_sc) return;  // uniform per workgroup
-  const int64_t wpb = pb * NW + w;
+  const int wblk = w / L::kWavesPerBlock;         // 64-pixel block in the run
+  const int t0 = (w % L::kWavesPerBlock) * TPW;   // first tile of this wave
+  const int64_t wpb = pb * (NW / L::kWavesPerBlock) + wblk;
   const bool live = wpb * kWavePix < P;  // waves past the grid still sync
 
-  double bf[KS][kTiles];
+  double bf[KS][TPW];
 #pragma unroll
   for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
-    for (int t = 0; t < kTiles; ++t)
+    for (int t = 0; t < TPW; ++t)
       bf[kk][t] = (live && kk < ks_real)
-                      ? cfrag[((wpb * ks_real + kk) * kTiles + t) * 64 + l]
+                      ? cfrag[((wpb * ks_real + kk) * kTiles + t0 + t) * 64 + l]
                       : 0.0;
 
   const bool scrub = flags & SF_EVAL_NAN_SCRUB;
@@ -314,28 +341,31 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
         af[kk] = (s < S && d < D) ? coef[s * D + d] : 0.0;
       }
     }
-    v4d acc[kTiles];
+    v4d acc[TPW];
 #pragma unroll
-    for (int t = 0; t < kTiles; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
+    for (int t = 0; t < TPW; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
-      for (int t = 0; t < kTiles; ++t)
+      for (int t = 0; t < TPW; ++t)
         acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[kk], bf[kk][t],
                                                       acc[t], 0, 0, 0);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      float red[kTiles];
+      float red[TPW];
 #pragma unroll
-      for (int t = 0; t < kTiles; ++t) {
+      for (int t = 0; t < TPW; ++t) {
         const double ph = acc[t][r];
         const double k = rint(ph * 0.15915494309189535);
         double x = fma(-k, 6.283185307179586, ph);
         x = fma(-k, 2.4492935982947064e-16, x);
         red[t] = (float)x;
       }
-      *reinterpret_cast<v4f*>(&buf[acc_row(l, r)][w * kWavePix + (l & 15) * kTiles]) =
-          v4f{red[0], red[1], red[2], red[3]};
+      float* dst = &buf[acc_row(l, r)][wblk * kWavePix + (l & 15) * kTiles + t0];
+      if (TPW == 4)
+        *reinterpret_cast<v4f*>(dst) = v4f{red[0], red[1], red[2 % TPW], red[3 % TPW]};
+      else
+        *reinterpret_cast<v2f*>(dst) = v2f{red[0], red[1 % TPW]};
     }
     __syncthreads();
     // ---- stores: wave w owns kSlotsPerWave slots of the group
@@ -351,7 +381,7 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float sn, cs;
-          sincosf(rv[e], &sn, &cs);
+          sincos_reduced(rv[e], sn, cs);
           if (scrub && isnan(cs)) cs = 1.0f;
           if (scrub && isnan(sn)) sn = 0.0f;
           if (be) {
@@ -389,7 +419,7 @@ int launch_cpix(sf_ctx* ctx, const double* d_x, const double* d_y) {
   return SF_OK;
 }
 
-template <int KS>
+template <int KS, int MINW>
 static int launch_eval_ks(sf_ctx* ctx, const double* coef,
                           const double* cxx, const double* cyy, int64_t S,
                           float* out, int64_t ring, unsigned flags) {
@@ -408,7 +438,7 @@ static int launch_eval_ks(sf_ctx* ctx, const double* coef,
   const bool nt = flags & SF_EVAL_NT_STORES;
   const bool gain = cxx != nullptr;
 #define SF_LAUNCH(V, F, N, G)                                                 \
-  hipLaunchKernelGGL((kl_eval_kernel<KS, V, F, N, G>), dim3((unsigned)nblk),  \
+  hipLaunchKernelGGL((kl_eval_kernel<KS, MINW, V, F, N, G>), dim3((unsigned)nblk),  \
                      dim3(256), 0, ctx->stream, ctx->d_cfrag, coef, cxx, cyy, \
                      ctx->D, S, P, n_pb, n_sc, groups, out, ring, flags)
 #define SF_LAUNCH_G(V, F, N) \
@@ -433,11 +463,11 @@ static int launch_eval_ks(sf_ctx* ctx, const double* coef,
   return SF_OK;
 }
 
-template <int KS, int NW>
+template <int KS, int NW, int TPW>
 static int launch_eval_lds(sf_ctx* ctx, const double* coef, int64_t S,
                            float* out, int64_t ring, unsigned flags) {
   const int64_t P = ctx->n_pix;
-  const int64_t run = EvalLds<NW>::kRun;
+  const int64_t run = EvalLds<NW, TPW>::kRun;
   const int64_t n_pb = (P + run - 1) / run;
   int groups = 16;
   while (groups > 1 && n_pb * ((S + 16 * groups - 1) / (16 * groups)) < 1024)
@@ -446,11 +476,11 @@ static int launch_eval_lds(sf_ctx* ctx, const double* coef, int64_t S,
   int64_t nblk = n_pb * n_sc;
   if ((n_pb & 7) == 0) nblk = ((nblk + 7) / 8) * 8;
   if (flags & SF_EVAL_NT_STORES)
-    hipLaunchKernelGGL((kl_eval_lds_kernel<KS, NW, true>), dim3((unsigned)nblk),
+    hipLaunchKernelGGL((kl_eval_lds_kernel<KS, NW, TPW, true>), dim3((unsigned)nblk),
                        dim3(64 * NW), 0, ctx->stream, ctx->d_cfrag, coef, ctx->D,
                        ctx->ksteps, S, P, n_pb, n_sc, groups, out, ring, flags);
   else
-    hipLaunchKernelGGL((kl_eval_lds_kernel<KS, NW, false>), dim3((unsigned)nblk),
+    hipLaunchKernelGGL((kl_eval_lds_kernel<KS, NW, TPW, false>), dim3((unsigned)nblk),
                        dim3(64 * NW), 0, ctx->stream, ctx->d_cfrag, coef, ctx->D,
                        ctx->ksteps, S, P, n_pb, n_sc, groups, out, ring, flags);
   SF_HIP(hipGetLastError());
@@ -465,15 +495,18 @@ int pick_eval_kernel(const sf_ctx* ctx, bool gain, unsigned flags,
   // screens, odd grids) takes the register-tile kernel
   const bool lds_ok = !gain && (flags & SF_EVAL_FAST_SINCOS) &&
                       (ctx->n_pix % 4 == 0) && out_aligned16;
+  const int opt = ctx->eval_kernel;
+  if (opt == SF_EVAL_KERNEL_TILE || opt == SF_EVAL_KERNEL_TILE3) return opt;
   if (!lds_ok) return SF_EVAL_KERNEL_TILE;
-  if (ctx->eval_kernel != SF_EVAL_KERNEL_AUTO) return ctx->eval_kernel;
+  if (opt != SF_EVAL_KERNEL_AUTO) return opt;
   // measured on MI355X (tools/eval_variants.py, profiles/round1d_eval_variants.txt):
   // long store runs win while the contraction is light; from ksteps 8 on
   // (D > 28) the per-group barrier serialises MFMA and stores and the
-  // register-tile kernel is faster
+  // register-tile kernel is faster, at 3 waves per SIMD from ksteps 10 on
+  // (D > 36: the Cpix fragments alone take 8*ksteps VGPRs)
   if (ctx->ksteps <= 2) return SF_EVAL_KERNEL_LDS4;
   if (ctx->ksteps <= 7) return SF_EVAL_KERNEL_LDS16;
-  return SF_EVAL_KERNEL_TILE;
+  return ctx->ksteps <= 9 ? SF_EVAL_KERNEL_TILE : SF_EVAL_KERNEL_TILE3;
 }
 
 template <int KS>
@@ -484,13 +517,19 @@ static int launch_eval_pick(sf_ctx* ctx, const double* coef, const double* cxx,
                                  (reinterpret_cast<uintptr_t>(out) & 15) == 0);
   switch (v) {
     case SF_EVAL_KERNEL_LDS4:
-      return launch_eval_lds<KS, 4>(ctx, coef, S, out, ring, flags);
+      return launch_eval_lds<KS, 4, 4>(ctx, coef, S, out, ring, flags);
     case SF_EVAL_KERNEL_LDS8:
-      return launch_eval_lds<KS, 8>(ctx, coef, S, out, ring, flags);
+      return launch_eval_lds<KS, 8, 4>(ctx, coef, S, out, ring, flags);
     case SF_EVAL_KERNEL_LDS16:
-      return launch_eval_lds<KS, 16>(ctx, coef, S, out, ring, flags);
+      return launch_eval_lds<KS, 16, 4>(ctx, coef, S, out, ring, flags);
+    case SF_EVAL_KERNEL_LDS8H:
+      return launch_eval_lds<KS, 8, 2>(ctx, coef, S, out, ring, flags);
+    case SF_EVAL_KERNEL_LDS16H:
+      return launch_eval_lds<KS, 16, 2>(ctx, coef, S, out, ring, flags);
+    case SF_EVAL_KERNEL_TILE3:
+      return launch_eval_ks<KS, 3>(ctx, coef, cxx, cyy, S, out, ring, flags);
     default:
-      return launch_eval_ks<KS>(ctx, coef, cxx, cyy, S, out, ring, flags);
+      return launch_eval_ks<KS, 2>(ctx, coef, cxx, cyy, S, out, ring, flags);
   }
 }
 

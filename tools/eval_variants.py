@@ -18,17 +18,20 @@ sys.path.insert(0, os.path.join(REPO, "ska-sdp-screen-fitting_amd"))
 from ska_sdp_screen_fitting_amd import get_context  # noqa: E402
 from ska_sdp_screen_fitting_amd._lib import (  # noqa: E402
     SF_EVAL_FAST_SINCOS, SF_EVAL_KERNEL_AUTO, SF_EVAL_KERNEL_LDS4,
-    SF_EVAL_KERNEL_LDS8, SF_EVAL_KERNEL_LDS16, SF_EVAL_KERNEL_TILE,
+    SF_EVAL_KERNEL_LDS8, SF_EVAL_KERNEL_LDS8H, SF_EVAL_KERNEL_LDS16,
+    SF_EVAL_KERNEL_LDS16H, SF_EVAL_KERNEL_TILE, SF_EVAL_KERNEL_TILE3,
     SF_EVAL_NAN_SCRUB, SF_EVAL_NT_STORES, SF_OPT_EVAL_KERNEL)
 
 KERNELS = {"auto": SF_EVAL_KERNEL_AUTO, "tile": SF_EVAL_KERNEL_TILE,
+           "tile3": SF_EVAL_KERNEL_TILE3,
            "lds4": SF_EVAL_KERNEL_LDS4, "lds8": SF_EVAL_KERNEL_LDS8,
-           "lds16": SF_EVAL_KERNEL_LDS16}
+           "lds16": SF_EVAL_KERNEL_LDS16, "lds8h": SF_EVAL_KERNEL_LDS8H,
+           "lds16h": SF_EVAL_KERNEL_LDS16H}
 
 ap = argparse.ArgumentParser()
 ap.add_argument("shapes", nargs="*", default=["20:256"])
 ap.add_argument("--variants", default=",".join(
-    f"{k}{s}" for k in KERNELS if k != "auto" for s in ("", "+nt")))
+    f"{k}+nt" for k in KERNELS))
 ap.add_argument("--reps", type=int, default=7)
 ap.add_argument("--slots", type=int, default=102400,
                 help="slots per launch at 256^2 (scaled by 256^2/N^2)")
@@ -89,6 +92,8 @@ for rep in range(args.reps):
         select(D, N, pp)
         ring = ring_bytes // (16 * N * N)
         out = out_flat[: ring * 4 * N * N].view(ring, 4, N, N)
+        ctx.set_option(SF_OPT_EVAL_KERNEL, SF_EVAL_KERNEL_AUTO)
+        ctx.eval(coef, S, out, ring, base)  # untimed: re-warm after select()
         for name, (kv, fl) in variants.items():
             ctx.set_option(SF_OPT_EVAL_KERNEL, kv)
             e0 = torch.cuda.Event(enable_timing=True)
