@@ -35,7 +35,11 @@ WORKLOADS = {
     "config3": (64, 100, 16, 20, 256, 0.01301),
     "config2-shape": (62, 20, 12, 7, 128, 0.02602),
     "config5-shape": (64, 100, 4, 50, 512, 0.006505),
+    # BASELINE.json configs[3]: the whole 256-ant array, sharded over the
+    # ranks (strong scaling); D = 20 as config 3
+    "config4": (256, 1000, 32, 20, 256, 0.01301),
 }
+STRONG = {"config4"}  # first field = stations of the whole job
 
 
 def parse():
@@ -190,9 +194,17 @@ def main():
                                                       make_solutions)
 
     A, T, F, D, N, cell = WORKLOADS[args.workload]
+    strong = args.workload in STRONG
+    if strong:
+        from ska_sdp_screen_fitting_amd.distributed import shard_range
+        A_total = A
+        a0, a1 = shard_range(A_total, world, rank)
+        A = a1 - a0
+    else:
+        A_total, a0 = A * world, A * rank
     sol = make_solutions(n_ant=A, n_time=T, n_freq=F, n_dir=D,
-                         ant_offset=A * rank, n_ant_total=A * world)
-    setup = setup_shard(sol, A * rank, A * world, FIELD_RA_DEG, FIELD_DEC_DEG,
+                         ant_offset=a0, n_ant_total=A_total)
+    setup = setup_shard(sol, a0, A_total, FIELD_RA_DEG, FIELD_DEC_DEG,
                         FIELD_WIDTH_DEG, cell,
                         device=coll_dev if world > 1 else "cpu")
     assert len(setup["x"]) == N
@@ -343,21 +355,22 @@ def main():
                 traffic = None
         line = {
             "metric": METRIC,
-            "value": S * world * args.steps / elapsed,
+            "value": T * F * A_total * args.steps / elapsed,
             "unit": "screen-slots/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
             "config": {
-                "workload": (f"{args.workload}: {A} ant x {T} time x {F} freq x "
-                             f"{D} dir per GPU (ant-sharded), KL {N}^2 screen, "
-                             "fit (phase, niter 2, adjust_order) + eval"),
+                "workload": (f"{args.workload}: {A_total} ant x {T} time x {F} freq x "
+                             f"{D} dir, {A} ant per GPU (ant-sharded, "
+                             f"{'strong' if strong else 'weak'} scaling), KL {N}^2 "
+                             "screen, fit (phase, niter 2, adjust_order) + eval"),
                 "slots_per_gpu": S, "grid": N, "n_dir": D,
                 "parallelism": f"ant-shard x{world}",
                 "eval_sincos": "fp64" if args.precise_sincos else "fp32-after-fp64-reduction",
