@@ -64,6 +64,9 @@ def parse():
     ap.add_argument("--reserve-cus", type=int, default=16,
                     help="compute units the eval stream leaves to the fit "
                          "stream (pipelined mode)")
+    ap.add_argument("--fit-on-reserved", type=int, default=0,
+                    help="1: confine the fit stream to the reserved CUs "
+                         "(pipelined mode)")
     ap.add_argument("--fit-priority", type=int, default=1,
                     help="1: fit stream at high priority (pipelined mode)")
     ap.add_argument("--eval-only", action="store_true",
@@ -239,7 +242,7 @@ def main():
     # --reserve-cus compute units (spread over the XCDs) to the fit stream, so
     # the fit of the next chunk is not starved by queued eval workgroups
     fit_stream = stream
-    masked_handle = None
+    masked_handle = fit_handle = None
     if n_chunks > 1:
         fit_stream = torch.cuda.Stream(dev, priority=-1 if args.fit_priority else 0)
         if args.reserve_cus > 0:
@@ -250,6 +253,10 @@ def main():
             reserved = [min(n_cu - 1, k * step + k % 8) for k in range(args.reserve_cus)]
             masked_handle = ctx.stream_create(reserved)
             stream = torch.cuda.ExternalStream(masked_handle, device=dev)
+            if args.fit_on_reserved:
+                keep = set(reserved)
+                fit_handle = ctx.stream_create([c for c in range(n_cu) if c not in keep])
+                fit_stream = torch.cuda.ExternalStream(fit_handle, device=dev)
 
     eval_kernel_name = ctx.eval_kernel(flags)
 
@@ -402,8 +409,9 @@ def main():
     # release the CU-masked stream before the HIP runtime tears down
     torch.cuda.synchronize(dev)
     ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
-    if masked_handle is not None:
-        ctx.stream_destroy(masked_handle)
+    for h in (masked_handle, fit_handle):
+        if h is not None:
+            ctx.stream_destroy(h)
     if world > 1:
         dist.destroy_process_group()
 

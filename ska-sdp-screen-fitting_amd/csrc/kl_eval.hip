@@ -527,7 +527,9 @@ static int launch_eval_pick(sf_ctx* ctx, const double* coef, const double* cxx,
     case SF_EVAL_KERNEL_LDS16H:
       return launch_eval_lds<KS, 16, 2>(ctx, coef, S, out, ring, flags);
     case SF_EVAL_KERNEL_TILE3:
-      return launch_eval_ks<KS, 3>(ctx, coef, cxx, cyy, S, out, ring, flags);
+      // below 8 k-steps the register tile fits 4 waves/SIMD anyway
+      return launch_eval_ks<KS, (KS >= 8 ? 3 : 2)>(ctx, coef, cxx, cyy, S, out,
+                                                   ring, flags);
     default:
       return launch_eval_ks<KS, 2>(ctx, coef, cxx, cyy, S, out, ring, flags);
   }

@@ -297,9 +297,9 @@ def test_eval_kernels_agree(ctx, dev, n_dir, grid):
     grids that are not a multiple of the store run, a NaN slot."""
     from ska_sdp_screen_fitting_amd import geometry
     from ska_sdp_screen_fitting_amd._lib import (
-        SF_EVAL_BIG_ENDIAN, SF_EVAL_FAST_SINCOS, SF_EVAL_KERNEL_AUTO,
-        SF_EVAL_KERNEL_LDS4, SF_EVAL_KERNEL_LDS8, SF_EVAL_KERNEL_LDS16,
-        SF_EVAL_KERNEL_TILE, SF_EVAL_NT_STORES, SF_OPT_EVAL_KERNEL)
+        EVAL_KERNEL_NAMES, SF_EVAL_BIG_ENDIAN, SF_EVAL_FAST_SINCOS,
+        SF_EVAL_KERNEL_AUTO, SF_EVAL_KERNEL_TILE, SF_EVAL_NT_STORES,
+        SF_OPT_EVAL_KERNEL)
     from ska_sdp_screen_fitting_amd.synthetic import make_solutions
     s = make_solutions(n_ant=2, n_time=2, n_freq=1, n_dir=n_dir, seed=4)
     pp, mra, mdec = geometry.piercepoints(s.dir_radec)
@@ -312,8 +312,7 @@ def test_eval_kernels_agree(ctx, dev, n_dir, grid):
     base = 1 | SF_EVAL_FAST_SINCOS
     outs = {}
     try:
-        for kv in (SF_EVAL_KERNEL_TILE, SF_EVAL_KERNEL_LDS4, SF_EVAL_KERNEL_LDS8,
-                   SF_EVAL_KERNEL_LDS16, SF_EVAL_KERNEL_AUTO):
+        for kv in sorted(EVAL_KERNEL_NAMES) + [SF_EVAL_KERNEL_AUTO]:
             ctx.set_option(SF_OPT_EVAL_KERNEL, kv)
             for extra in (0, SF_EVAL_NT_STORES, SF_EVAL_BIG_ENDIAN):
                 o = gpu_eval(ctx, dev, pp, x, y, coef, flags=base | extra)
