@@ -4,7 +4,8 @@ BASELINE.json metric) on the reference fixture:
 
   config 1: tessellated, 0.2 deg cells (17^2), smooth 0.1 deg
   config 2: KL, 128^2 grid (cellsize 0.02602)
-  (optional) KL 256^2 on the fixture
+  (optional) KL 256^2 on the fixture; config3-10t = the first 10 time slots
+  of config 3 (synthetic, 10.7 GB cube)
 
 Prints one JSON line per case: wall-clock of make_aterm_image (fit + eval +
 FITS write, host I/O included) and the cube size.
@@ -27,24 +28,45 @@ CASES = {
     "config1": ("tessellated", 0.2, 0.1),
     "config2": ("kl", 0.02602, 0.0),
     "kl256": ("kl", 0.01301, 0.0),
+    # config 3 (64 ant x 100 t x 16 f x 20 dir, 256^2) is a 107 GB cube; this
+    # case writes its first 10 time slots (10.7 GB) from the same synthetic
+    # generator as bench.py
+    "config3-10t": ("kl", 0.01301, 0.0),
 }
+SYNTH = {"config3-10t": (64, 10, 16, 20)}
 
 
-def run(name, outdir):
+def synthetic_npz(name, outdir):
+    """Synthetic solutions of a SYNTH case as a .npz H5parm stand-in."""
+    import numpy as np
+    from ska_sdp_screen_fitting_amd.synthetic import make_solutions
+    A, T, F, D = SYNTH[name]
+    sol = make_solutions(n_ant=A, n_time=T, n_freq=F, n_dir=D)
+    path = os.path.join(outdir, f"{name}_solutions.npz")
+    np.savez(path, val=sol.val, weight=sol.weight, times=sol.times,
+             freqs=sol.freqs, ant_names=np.array(sol.ant_names),
+             ant_pos=sol.ant_pos, dir_names=np.array(sol.dir_names),
+             dir_radec=sol.dir_radec)
+    return path, A * T * F
+
+
+def run(name, outdir, h5=None, slots=14880):
     st, cell, smooth = CASES[name]
     outroot = os.path.join(outdir, name)
+    sky = SKY if h5 is None else None
     t0 = time.perf_counter()
-    make_aterm_image(FIX, soltabname="phase000", screen_type=st, outroot=outroot,
+    make_aterm_image(h5 or FIX, soltabname="phase000", screen_type=st,
+                     outroot=outroot,
                      bounds_deg=[124.565, 66.165, 127.895, 62.835],
-                     bounds_mid_deg=[126.23, 64.50], skymodel=SKY,
+                     bounds_mid_deg=[126.23, 64.50], skymodel=sky,
                      padding_fraction=0, cellsize_deg=cell, smooth_deg=smooth,
                      ncpu=0)
     dt = time.perf_counter() - t0
     size = sum(os.path.getsize(os.path.join(outdir, f)) for f in os.listdir(outdir)
                if f.startswith(name) and f.endswith(".fits"))
     return {"case": name, "screen_type": st, "cellsize_deg": cell,
-            "wall_s": dt, "fits_bytes": size, "slots": 14880,
-            "slots_per_s": 14880 / dt}
+            "wall_s": dt, "fits_bytes": size, "slots": slots,
+            "slots_per_s": slots / dt, "fits_GB_per_s": size / dt / 1e9}
 
 
 def main():
@@ -54,11 +76,13 @@ def main():
     ap.add_argument("--repeat", type=int, default=2)
     a = ap.parse_args()
     for name in a.cases:
-        for k in range(a.repeat):
-            with tempfile.TemporaryDirectory(dir=a.outdir) as d:
-                r = run(name, d)
-            r["repeat"] = k
-            print(json.dumps(r), flush=True)
+        with tempfile.TemporaryDirectory(dir=a.outdir) as src:
+            h5, slots = synthetic_npz(name, src) if name in SYNTH else (None, 14880)
+            for k in range(a.repeat):
+                with tempfile.TemporaryDirectory(dir=a.outdir) as d:
+                    r = run(name, d, h5, slots)
+                r["repeat"] = k
+                print(json.dumps(r), flush=True)
 
 
 if __name__ == "__main__":
