@@ -38,6 +38,9 @@ WORKLOADS = {
     # BASELINE.json configs[3]: the whole 256-ant array, sharded over the
     # ranks (strong scaling); D = 20 as config 3
     "config4": (256, 1000, 32, 20, 256, 0.01301),
+    # BASELINE.json configs[4] (SKA-Low scale): 64 of its 512 stations per
+    # GPU, so --gpus 8 is the whole 512 ant x 4000 t x 64 f x 50 dir array
+    "config5": (64, 4000, 64, 50, 512, 0.006505),
 }
 STRONG = {"config4"}  # first field = stations of the whole job
 
@@ -137,7 +140,7 @@ def cpu_baseline(sol, setup, n_workers, slots_fit=64, slots_eval=192):
         "cores": n_workers,
         "kind": "port",
         "sample": (f"oracle (numpy fp64 restatement) on {n_fit} fit slots and "
-                   f"{n_ev} 256^2 eval slots of the same workload, "
+                   f"{n_ev} {len(setup['x'])}^2 eval slots of the same workload, "
                    f"{n_workers} single-threaded workers, {wall:.1f} s wall; "
                    f"fit {t_fit / n_fit * 1e3:.3f} ms/slot/core, eval "
                    f"{t_ev / n_ev * 1e3:.1f} ms/slot/core"),

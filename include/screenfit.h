@@ -109,6 +109,10 @@ int sf_device_cus(sf_ctx* ctx, int* n_cu);
  * screens), LDS4 / LDS8 / LDS16 = LDS-staged stores with 1 / 2 / 4 KiB
  * contiguous runs per (slot, plane). */
 #define SF_OPT_EVAL_KERNEL 2
+/* SF_OPT_EVAL_MAX_BLOCKS caps the workgroups of an evaluation launch (0 =
+ * the dispatch limit); each workgroup then walks several (pixel block, slot
+ * chunk) items.  For tests of that walk. */
+#define SF_OPT_EVAL_MAX_BLOCKS 3
 #define SF_EVAL_KERNEL_AUTO 0
 #define SF_EVAL_KERNEL_TILE 1
 #define SF_EVAL_KERNEL_LDS4 2

@@ -99,6 +99,26 @@ __device__ __forceinline__ void sincos_reduced(float r, float& s, float& c) {
   c = ((iq + 1) & 2) ? -b : b;
 }
 
+// Workgroup index -> (pixel block, slot chunk).  XCD-aware when the pixel
+// blocks divide by 8: consecutive workgroups go to the 8 XCDs round-robin,
+// so XCD x owns pixel blocks [x*per, (x+1)*per) and their Cpix slices stay
+// in its L2.  The eval kernels walk bb = blockIdx.x, += gridDim.x (a
+// multiple of 8, so a workgroup stays on its XCD's pixel blocks): one HSA
+// dispatch counts at most 2^32 work-items, which config 5 (16 M slots per
+// GPU at 512^2) would exceed with one workgroup per (pixel block, chunk).
+__device__ __forceinline__ void eval_block(int64_t bb, int64_t n_pb,
+                                           int64_t& pb, int64_t& sc) {
+  if ((n_pb & 7) == 0) {
+    const int64_t per = n_pb >> 3;
+    const int64_t x = bb & 7, i = bb >> 3;
+    pb = x * per + (i % per);
+    sc = i / per;
+  } else {
+    pb = bb % n_pb;
+    sc = bb / n_pb;
+  }
+}
+
 template <bool FAST>
 __device__ __forceinline__ void jones_sincos(double ph, float& s, float& c) {
   if (FAST) {
@@ -144,125 +164,119 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
   const int l = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   // XCD-aware block -> (pixel block, slot chunk)
-  const int64_t b = blockIdx.x;
-  int64_t pb, sc;
-  if ((n_pb & 7) == 0) {
-    const int64_t per = n_pb >> 3;
-    const int64_t x = b & 7, i = b >> 3;
-    pb = x * per + (i % per);
-    sc = i / per;
-  } else {
-    pb = b % n_pb;
-    sc = b / n_pb;
-  }
-  if (sc >= n_sc) return;
-  const int64_t wpb = pb * kEvalWaves + w;
-  const int64_t p0 = wpb * kWavePix + (int64_t)(l & 15) * kTiles;
-  if (wpb * kWavePix >= P) return;
+  const int64_t n_blocks = n_pb * n_sc;
+  for (int64_t bb = blockIdx.x; bb < n_blocks; bb += gridDim.x) {
+    int64_t pb, sc;
+    eval_block(bb, n_pb, pb, sc);
+    if (sc >= n_sc) continue;
+    const int64_t wpb = pb * kEvalWaves + w;
+    const int64_t p0 = wpb * kWavePix + (int64_t)(l & 15) * kTiles;
+    if (wpb * kWavePix >= P) continue;
 
-  double bf[KS][kTiles];
-#pragma unroll
-  for (int kk = 0; kk < KS; ++kk)
-#pragma unroll
-    for (int t = 0; t < kTiles; ++t)
-      bf[kk][t] = cfrag[((wpb * KS + kk) * kTiles + t) * 64 + l];
-
-  const bool scrub = flags & SF_EVAL_NAN_SCRUB;
-  const bool be = flags & SF_EVAL_BIG_ENDIAN;
-  const int64_t slot_base = sc * (int64_t)chunk_groups * 16;
-  for (int g = 0; g < chunk_groups; ++g) {
-    const int64_t s0 = slot_base + (int64_t)g * 16;
-    if (s0 >= S) break;
-    double af[KS];
-    {
-      const int64_t s = s0 + (l & 15);
-#pragma unroll
-      for (int kk = 0; kk < KS; ++kk) {
-        const int d = 4 * kk + (l >> 4);
-        af[kk] = (s < S && d < D) ? coef[s * D + d] : 0.0;
-      }
-    }
-    v4d acc[kTiles];
-#pragma unroll
-    for (int t = 0; t < kTiles; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
+    double bf[KS][kTiles];
 #pragma unroll
     for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
       for (int t = 0; t < kTiles; ++t)
-        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[kk], bf[kk][t],
-                                                      acc[t], 0, 0, 0);
-    // gain: the XX / YY log-amplitude screens share the pixel basis
-    v4d accx[GAIN ? kTiles : 1], accy[GAIN ? kTiles : 1];
-    if (GAIN) {
-      const int64_t s = s0 + (l & 15);
+        bf[kk][t] = cfrag[((wpb * KS + kk) * kTiles + t) * 64 + l];
+
+    const bool scrub = flags & SF_EVAL_NAN_SCRUB;
+    const bool be = flags & SF_EVAL_BIG_ENDIAN;
+    const int64_t slot_base = sc * (int64_t)chunk_groups * 16;
+    for (int g = 0; g < chunk_groups; ++g) {
+      const int64_t s0 = slot_base + (int64_t)g * 16;
+      if (s0 >= S) break;
+      double af[KS];
+      {
+        const int64_t s = s0 + (l & 15);
 #pragma unroll
-      for (int t = 0; t < kTiles; ++t) {
-        accx[t] = v4d{0.0, 0.0, 0.0, 0.0};
-        accy[t] = v4d{0.0, 0.0, 0.0, 0.0};
+        for (int kk = 0; kk < KS; ++kk) {
+          const int d = 4 * kk + (l >> 4);
+          af[kk] = (s < S && d < D) ? coef[s * D + d] : 0.0;
+        }
       }
+      v4d acc[kTiles];
 #pragma unroll
-      for (int kk = 0; kk < KS; ++kk) {
-        const int d = 4 * kk + (l >> 4);
-        const bool ok = s < S && d < D;
-        const double ax = ok ? coef_xx[s * D + d] : 0.0;
-        const double ay = ok ? coef_yy[s * D + d] : 0.0;
+      for (int t = 0; t < kTiles; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+        for (int t = 0; t < kTiles; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[kk], bf[kk][t],
+                                                        acc[t], 0, 0, 0);
+      // gain: the XX / YY log-amplitude screens share the pixel basis
+      v4d accx[GAIN ? kTiles : 1], accy[GAIN ? kTiles : 1];
+      if (GAIN) {
+        const int64_t s = s0 + (l & 15);
 #pragma unroll
         for (int t = 0; t < kTiles; ++t) {
-          accx[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ax, bf[kk][t], accx[t], 0, 0, 0);
-          accy[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ay, bf[kk][t], accy[t], 0, 0, 0);
+          accx[t] = v4d{0.0, 0.0, 0.0, 0.0};
+          accy[t] = v4d{0.0, 0.0, 0.0, 0.0};
+        }
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) {
+          const int d = 4 * kk + (l >> 4);
+          const bool ok = s < S && d < D;
+          const double ax = ok ? coef_xx[s * D + d] : 0.0;
+          const double ay = ok ? coef_yy[s * D + d] : 0.0;
+#pragma unroll
+          for (int t = 0; t < kTiles; ++t) {
+            accx[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ax, bf[kk][t], accx[t], 0, 0, 0);
+            accy[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ay, bf[kk][t], accy[t], 0, 0, 0);
+          }
         }
       }
-    }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t s = s0 + acc_row(l, r);
-      if (s >= S) continue;
-      // planes 0..3 = Re XX, Im XX, Re YY, Im YY
-      float pv[4][kTiles];
+      for (int r = 0; r < 4; ++r) {
+        const int64_t s = s0 + acc_row(l, r);
+        if (s >= S) continue;
+        // planes 0..3 = Re XX, Im XX, Re YY, Im YY
+        float pv[4][kTiles];
 #pragma unroll
-      for (int t = 0; t < kTiles; ++t) {
-        float sf, cf;
-        jones_sincos<FAST>(acc[t][r], sf, cf);
-        if (GAIN) {
-          // reference: A (fp64) * cos (fp64), one cast at the FITS store
-          const double ax = amp10<FAST>(accx[t][r]);
-          const double ay = amp10<FAST>(accy[t][r]);
-          pv[0][t] = (float)(ax * (double)cf);
-          pv[1][t] = (float)(ax * (double)sf);
-          pv[2][t] = (float)(ay * (double)cf);
-          pv[3][t] = (float)(ay * (double)sf);
-        } else {
-          pv[0][t] = pv[2][t] = cf;
-          pv[1][t] = pv[3][t] = sf;
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          if (scrub && isnan(pv[q][t])) pv[q][t] = (q & 1) ? 0.0f : 1.0f;
-          if (be) pv[q][t] = bswapf(pv[q][t]);
-        }
-      }
-      float* o = out + ((s % ring) * 4) * P + p0;
-      if (VEC4) {
-        // P % 4 == 0: a lane's 4 pixels are all inside the grid or all out
-        // (the last wave block of a grid that is not a multiple of 64)
-        if (p0 < P) {
+        for (int t = 0; t < kTiles; ++t) {
+          float sf, cf;
+          jones_sincos<FAST>(acc[t][r], sf, cf);
+          if (GAIN) {
+            // reference: A (fp64) * cos (fp64), one cast at the FITS store
+            const double ax = amp10<FAST>(accx[t][r]);
+            const double ay = amp10<FAST>(accy[t][r]);
+            pv[0][t] = (float)(ax * (double)cf);
+            pv[1][t] = (float)(ax * (double)sf);
+            pv[2][t] = (float)(ay * (double)cf);
+            pv[3][t] = (float)(ay * (double)sf);
+          } else {
+            pv[0][t] = pv[2][t] = cf;
+            pv[1][t] = pv[3][t] = sf;
+          }
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const v4f v = {pv[q][0], pv[q][1], pv[q][2], pv[q][3]};
-            store4<NT>(o + q * P, v);
+            if (scrub && isnan(pv[q][t])) pv[q][t] = (q & 1) ? 0.0f : 1.0f;
+            if (be) pv[q][t] = bswapf(pv[q][t]);
           }
         }
-      } else {
+        float* o = out + ((s % ring) * 4) * P + p0;
+        if (VEC4) {
+          // P % 4 == 0: a lane's 4 pixels are all inside the grid or all out
+          // (the last wave block of a grid that is not a multiple of 64)
+          if (p0 < P) {
 #pragma unroll
-        for (int t = 0; t < kTiles; ++t) {
-          if (p0 + t < P) {
+            for (int q = 0; q < 4; ++q) {
+              const v4f v = {pv[q][0], pv[q][1], pv[q][2], pv[q][3]};
+              store4<NT>(o + q * P, v);
+            }
+          }
+        } else {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) o[q * P + t] = pv[q][t];
+          for (int t = 0; t < kTiles; ++t) {
+            if (p0 + t < P) {
+#pragma unroll
+              for (int q = 0; q < 4; ++q) o[q * P + t] = pv[q][t];
+            }
           }
         }
       }
     }
-  }
+  }  // workgroup walk
 }
 
 // LDS-staged variant (phase screens, fp32 sincos epilogue): the same MFMA
@@ -297,115 +311,125 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
   __shared__ float tile[2][16][L::kStride];
   const int l = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
-  const int64_t b = blockIdx.x;
-  int64_t pb, sc;
-  if ((n_pb & 7) == 0) {
-    const int64_t per = n_pb >> 3;
-    const int64_t x = b & 7, i = b >> 3;
-    pb = x * per + (i % per);
-    sc = i / per;
-  } else {
-    pb = b % n_pb;
-    sc = b / n_pb;
-  }
-  if (sc >= n_sc) return;  // uniform per workgroup
-  const int wblk = w / L::kWavesPerBlock;         // 64-pixel block in the run
-  const int t0 = (w % L::kWavesPerBlock) * TPW;   // first tile of this wave
-  const int64_t wpb = pb * (NW / L::kWavesPerBlock) + wblk;
-  const bool live = wpb * kWavePix < P;  // waves past the grid still sync
+  const int64_t n_blocks = n_pb * n_sc;
+  for (int64_t bb = blockIdx.x; bb < n_blocks; bb += gridDim.x) {
+    int64_t pb, sc;
+    eval_block(bb, n_pb, pb, sc);
+    if (sc >= n_sc) continue;  // uniform per workgroup
+    const int wblk = w / L::kWavesPerBlock;         // 64-pixel block in the run
+    const int t0 = (w % L::kWavesPerBlock) * TPW;   // first tile of this wave
+    const int64_t wpb = pb * (NW / L::kWavesPerBlock) + wblk;
+    const bool live = wpb * kWavePix < P;  // waves past the grid still sync
 
-  double bf[KS][TPW];
-#pragma unroll
-  for (int kk = 0; kk < KS; ++kk)
-#pragma unroll
-    for (int t = 0; t < TPW; ++t)
-      bf[kk][t] = (live && kk < ks_real)
-                      ? cfrag[((wpb * ks_real + kk) * kTiles + t0 + t) * 64 + l]
-                      : 0.0;
-
-  const bool scrub = flags & SF_EVAL_NAN_SCRUB;
-  const bool be = flags & SF_EVAL_BIG_ENDIAN;
-  const int64_t pix0 = pb * L::kRun;
-  const int64_t slot_base = sc * (int64_t)chunk_groups * 16;
-  for (int g = 0; g < chunk_groups; ++g) {
-    const int64_t s0 = slot_base + (int64_t)g * 16;
-    if (s0 >= S) break;  // uniform per workgroup
-    float(*buf)[L::kStride] = tile[g & 1];
-    // ---- contraction: 16 slots x this wave's 64 pixels
-    double af[KS];
-    {
-      const int64_t s = s0 + (l & 15);
-#pragma unroll
-      for (int kk = 0; kk < KS; ++kk) {
-        const int d = 4 * kk + (l >> 4);
-        af[kk] = (s < S && d < D) ? coef[s * D + d] : 0.0;
-      }
-    }
-    v4d acc[TPW];
-#pragma unroll
-    for (int t = 0; t < TPW; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
+    double bf[KS][TPW];
 #pragma unroll
     for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
       for (int t = 0; t < TPW; ++t)
-        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[kk], bf[kk][t],
-                                                      acc[t], 0, 0, 0);
+        bf[kk][t] = (live && kk < ks_real)
+                        ? cfrag[((wpb * ks_real + kk) * kTiles + t0 + t) * 64 + l]
+                        : 0.0;
+
+    const bool scrub = flags & SF_EVAL_NAN_SCRUB;
+    const bool be = flags & SF_EVAL_BIG_ENDIAN;
+    const int64_t pix0 = pb * L::kRun;
+    const int64_t slot_base = sc * (int64_t)chunk_groups * 16;
+    for (int g = 0; g < chunk_groups; ++g) {
+      const int64_t s0 = slot_base + (int64_t)g * 16;
+      if (s0 >= S) break;  // uniform per workgroup
+      float(*buf)[L::kStride] = tile[g & 1];
+      // ---- contraction: 16 slots x this wave's 64 pixels
+      double af[KS];
+      {
+        const int64_t s = s0 + (l & 15);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float red[TPW];
-#pragma unroll
-      for (int t = 0; t < TPW; ++t) {
-        const double ph = acc[t][r];
-        const double k = rint(ph * 0.15915494309189535);
-        double x = fma(-k, 6.283185307179586, ph);
-        x = fma(-k, 2.4492935982947064e-16, x);
-        red[t] = (float)x;
-      }
-      float* dst = &buf[acc_row(l, r)][wblk * kWavePix + (l & 15) * kTiles + t0];
-      if (TPW == 4)
-        *reinterpret_cast<v4f*>(dst) = v4f{red[0], red[1], red[2 % TPW], red[3 % TPW]};
-      else
-        *reinterpret_cast<v2f*>(dst) = v2f{red[0], red[1 % TPW]};
-    }
-    __syncthreads();
-    // ---- stores: wave w owns kSlotsPerWave slots of the group
-#pragma unroll
-    for (int j = 0; j < L::kSlotsPerWave; ++j) {
-      const int row = w * L::kSlotsPerWave + j;
-      const int64_t s = s0 + row;
-      if (s >= S) break;
-      float cv[L::kChunks][4], sv[L::kChunks][4];
-#pragma unroll
-      for (int c = 0; c < L::kChunks; ++c) {
-        const v4f rv = *reinterpret_cast<const v4f*>(&buf[row][c * 256 + 4 * l]);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float sn, cs;
-          sincos_reduced(rv[e], sn, cs);
-          if (scrub && isnan(cs)) cs = 1.0f;
-          if (scrub && isnan(sn)) sn = 0.0f;
-          if (be) {
-            cs = bswapf(cs);
-            sn = bswapf(sn);
-          }
-          cv[c][e] = cs;
-          sv[c][e] = sn;
+        for (int kk = 0; kk < KS; ++kk) {
+          const int d = 4 * kk + (l >> 4);
+          af[kk] = (s < S && d < D) ? coef[s * D + d] : 0.0;
         }
       }
-      float* o = out + ((s % ring) * 4) * P + pix0 + 4 * l;
+      v4d acc[TPW];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int t = 0; t < TPW; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+        for (int t = 0; t < TPW; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[kk], bf[kk][t],
+                                                        acc[t], 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float red[TPW];
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+          const double ph = acc[t][r];
+          const double k = rint(ph * 0.15915494309189535);
+          double x = fma(-k, 6.283185307179586, ph);
+          x = fma(-k, 2.4492935982947064e-16, x);
+          red[t] = (float)x;
+        }
+        float* dst = &buf[acc_row(l, r)][wblk * kWavePix + (l & 15) * kTiles + t0];
+        if (TPW == 4)
+          *reinterpret_cast<v4f*>(dst) = v4f{red[0], red[1], red[2 % TPW], red[3 % TPW]};
+        else
+          *reinterpret_cast<v2f*>(dst) = v2f{red[0], red[1 % TPW]};
+      }
+      __syncthreads();
+      // ---- stores: wave w owns kSlotsPerWave slots of the group
+#pragma unroll
+      for (int j = 0; j < L::kSlotsPerWave; ++j) {
+        const int row = w * L::kSlotsPerWave + j;
+        const int64_t s = s0 + row;
+        if (s >= S) break;
+        float cv[L::kChunks][4], sv[L::kChunks][4];
 #pragma unroll
         for (int c = 0; c < L::kChunks; ++c) {
-          if (pix0 + c * 256 + 4 * l < P) {
-            const v4f v = (q & 1) ? v4f{sv[c][0], sv[c][1], sv[c][2], sv[c][3]}
-                                  : v4f{cv[c][0], cv[c][1], cv[c][2], cv[c][3]};
-            store4<NT>(o + q * P + c * 256, v);
+          const v4f rv = *reinterpret_cast<const v4f*>(&buf[row][c * 256 + 4 * l]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float sn, cs;
+            sincos_reduced(rv[e], sn, cs);
+            if (scrub && isnan(cs)) cs = 1.0f;
+            if (scrub && isnan(sn)) sn = 0.0f;
+            if (be) {
+              cs = bswapf(cs);
+              sn = bswapf(sn);
+            }
+            cv[c][e] = cs;
+            sv[c][e] = sn;
+          }
+        }
+        float* o = out + ((s % ring) * 4) * P + pix0 + 4 * l;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+#pragma unroll
+          for (int c = 0; c < L::kChunks; ++c) {
+            if (pix0 + c * 256 + 4 * l < P) {
+              const v4f v = (q & 1) ? v4f{sv[c][0], sv[c][1], sv[c][2], sv[c][3]}
+                                    : v4f{cv[c][0], cv[c][1], cv[c][2], cv[c][3]};
+              store4<NT>(o + q * P + c * 256, v);
+            }
           }
         }
       }
     }
-  }
+    // the next workgroup item reuses the LDS tiles from buffer 0
+    __syncthreads();
+  }  // workgroup walk
+}
+
+// Grid of an eval launch: one workgroup per (pixel block, slot chunk) up to
+// the dispatch limit of 2^32 work-items (kept at 2^31), a multiple of 8 so
+// the XCD mapping of eval_block holds for every item a workgroup walks.
+static int64_t eval_grid(const sf_ctx* ctx, int64_t n_pb, int64_t n_sc,
+                         int threads) {
+  int64_t n = n_pb * n_sc;
+  if ((n_pb & 7) == 0) n = ((n + 7) / 8) * 8;
+  int64_t cap = ((int64_t)1 << 31) / threads;
+  if (ctx->eval_max_blocks > 0 && ctx->eval_max_blocks < cap)
+    cap = ctx->eval_max_blocks;
+  cap = cap < 8 ? 8 : cap & ~(int64_t)7;
+  return n < cap ? n : cap;
 }
 
 int launch_cpix(sf_ctx* ctx, const double* d_x, const double* d_y) {
@@ -431,8 +455,7 @@ static int launch_eval_ks(sf_ctx* ctx, const double* coef,
   while (groups > 1 && n_pb * ((S + 16 * groups - 1) / (16 * groups)) < 2048)
     groups >>= 1;
   const int64_t n_sc = (S + 16 * groups - 1) / (16 * groups);
-  int64_t nblk = n_pb * n_sc;
-  if ((n_pb & 7) == 0) nblk = ((nblk + 7) / 8) * 8;
+  const int64_t nblk = eval_grid(ctx, n_pb, n_sc, 256);
   const bool vec4 = (P % 4 == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
   const bool fast = flags & SF_EVAL_FAST_SINCOS;
   const bool nt = flags & SF_EVAL_NT_STORES;
@@ -473,8 +496,7 @@ static int launch_eval_lds(sf_ctx* ctx, const double* coef, int64_t S,
   while (groups > 1 && n_pb * ((S + 16 * groups - 1) / (16 * groups)) < 1024)
     groups >>= 1;
   const int64_t n_sc = (S + 16 * groups - 1) / (16 * groups);
-  int64_t nblk = n_pb * n_sc;
-  if ((n_pb & 7) == 0) nblk = ((nblk + 7) / 8) * 8;
+  const int64_t nblk = eval_grid(ctx, n_pb, n_sc, 64 * NW);
   if (flags & SF_EVAL_NT_STORES)
     hipLaunchKernelGGL((kl_eval_lds_kernel<KS, NW, TPW, true>), dim3((unsigned)nblk),
                        dim3(64 * NW), 0, ctx->stream, ctx->d_cfrag, coef, ctx->D,

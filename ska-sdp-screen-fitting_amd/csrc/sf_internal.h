@@ -85,6 +85,7 @@ struct sf_ctx {
   int force_general = 0;
   // evaluation kernel (SF_OPT_EVAL_KERNEL)
   int eval_kernel = SF_EVAL_KERNEL_AUTO;
+  int64_t eval_max_blocks = 0;  // SF_OPT_EVAL_MAX_BLOCKS (0 = dispatch limit)
 };
 
 namespace sf {

@@ -299,7 +299,7 @@ def test_eval_kernels_agree(ctx, dev, n_dir, grid):
     from ska_sdp_screen_fitting_amd._lib import (
         EVAL_KERNEL_NAMES, SF_EVAL_BIG_ENDIAN, SF_EVAL_FAST_SINCOS,
         SF_EVAL_KERNEL_AUTO, SF_EVAL_KERNEL_TILE, SF_EVAL_NT_STORES,
-        SF_OPT_EVAL_KERNEL)
+        SF_OPT_EVAL_KERNEL, SF_OPT_EVAL_MAX_BLOCKS)
     from ska_sdp_screen_fitting_amd.synthetic import make_solutions
     s = make_solutions(n_ant=2, n_time=2, n_freq=1, n_dir=n_dir, seed=4)
     pp, mra, mdec = geometry.piercepoints(s.dir_radec)
@@ -319,8 +319,14 @@ def test_eval_kernels_agree(ctx, dev, n_dir, grid):
                 if extra == SF_EVAL_BIG_ENDIAN:
                     o = o.byteswap()
                 outs[(kv, extra)] = o
+            # 8 workgroups walking every (pixel block, slot chunk) item: the
+            # path large launches take past the 2^32 work-item dispatch limit
+            ctx.set_option(SF_OPT_EVAL_MAX_BLOCKS, 8)
+            outs[(kv, "walk")] = gpu_eval(ctx, dev, pp, x, y, coef, flags=base)
+            ctx.set_option(SF_OPT_EVAL_MAX_BLOCKS, 0)
     finally:
         ctx.set_option(SF_OPT_EVAL_KERNEL, SF_EVAL_KERNEL_AUTO)
+        ctx.set_option(SF_OPT_EVAL_MAX_BLOCKS, 0)
     ref = outs[(SF_EVAL_KERNEL_TILE, 0)]
     for k, o in outs.items():
         assert np.array_equal(o.view(np.int32), ref.view(np.int32)), k
