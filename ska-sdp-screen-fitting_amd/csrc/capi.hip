@@ -275,7 +275,12 @@ int sf_kl_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,
   SF_REQUIRE(p->screen_type == SF_SCREEN_PHASE || p->screen_type == SF_SCREEN_TEC ||
                  p->screen_type == SF_SCREEN_AMPLITUDE,
              SF_EINVAL, "sf_kl_fit: unsupported screen type");
-  SF_REQUIRE(p->niter >= 1, SF_EINVAL, "sf_kl_fit: niter must be >= 1");
+  SF_REQUIRE(p->niter >= 1 && p->niter <= 64, SF_EINVAL,
+             "sf_kl_fit: niter must be in [1, 64]");
+  // the mask hash table holds (2 niter + 2) entries per slot in int indices
+  SF_REQUIRE((int64_t)T * F * A * (2 * p->niter + 2) < ((int64_t)1 << 30),
+             SF_EINVAL,
+             "sf_kl_fit: too many slots for one call (split the time axis)");
   SF_REQUIRE(p->ref_ant >= -1 && p->ant_offset >= 0, SF_EINVAL,
              "sf_kl_fit: bad ref_ant / ant_offset");
   {

@@ -33,6 +33,7 @@
 namespace sf {
 
 constexpr double kAtol = 1e-3;             // pinv(rcond=1e-3)
+constexpr size_t kLdsBytes = 160 * 1024;   // LDS of one gfx950 CU
 constexpr double kTinyW = 1e-3 * 1.001;    // slow-path threshold on weights
 constexpr unsigned long long kEmptyKey = 0ull;
 
@@ -788,8 +789,19 @@ static int launch_pass(sf_ctx* ctx, int it, const sf_fit_params* p,
   const int D = ctx->D;
   const size_t shared = fast_shared_bytes(D);
   const size_t wave = fast_wave_bytes(D, SLOW);
-  int nw = 4;
-  while (nw > 1 && shared + nw * wave > 64 * 1024) --nw;
+  // waves per workgroup (<= 4): the most resident waves per CU under the
+  // 160 KiB LDS of a gfx950 CU (the per-wave subset basis is D^2 doubles, so
+  // at D = 50 only 2 waves fit; the smaller workgroup wins ties)
+  int nw = 1, best = 0;
+  for (int k = 1; k <= 4; ++k) {
+    const size_t per_wg = shared + k * wave;
+    if (per_wg > kLdsBytes) break;
+    const int waves = k * (int)(kLdsBytes / per_wg);
+    if (waves > best) {
+      best = waves;
+      nw = k;
+    }
+  }
   const size_t shm = shared + nw * wave;
   if (shm > 64 * 1024)
     SF_HIP(hipFuncSetAttribute(
