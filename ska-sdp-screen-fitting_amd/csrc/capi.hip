@@ -228,6 +228,11 @@ int sf_set_basis(sf_ctx* ctx, const double* pp, int D, double r0,
   SF_REQUIRE(r0 > 0.0, SF_EINVAL, "sf_set_basis: r0 must be > 0");
   SF_HIP(hipSetDevice(ctx->device));
   SF_HIP(hipStreamSynchronize(ctx->stream));
+  // invalidate basis and grid until the new basis is complete: a failure
+  // below must not leave a context whose D points at freed buffers
+  ctx->D = 0;
+  ctx->nx = ctx->ny = 0;
+  ctx->n_pix = 0;
   SF_TRY(dev_alloc(&ctx->d_pp, (size_t)3 * D));
   SF_TRY(dev_alloc(&ctx->d_c, (size_t)D * D));
   SF_TRY(dev_alloc(&ctx->d_pinv, (size_t)D * D));
@@ -239,12 +244,13 @@ int sf_set_basis(sf_ctx* ctx, const double* pp, int D, double r0,
   ctx->D = D;
   ctx->r0 = r0;
   ctx->beta = beta;
-  // the grid (if any) belongs to the previous basis
-  ctx->nx = ctx->ny = 0;
-  ctx->n_pix = 0;
-  SF_TRY(sf::launch_basis(ctx));
-  SF_HIP(hipStreamSynchronize(ctx->stream));
-  return SF_OK;
+  int rc = sf::launch_basis(ctx);
+  if (rc == SF_OK && hipStreamSynchronize(ctx->stream) != hipSuccess) {
+    set_error("sf_set_basis: basis kernel failed");
+    rc = SF_EIO;
+  }
+  if (rc != SF_OK) ctx->D = 0;
+  return rc;
 }
 
 int sf_get_basis(sf_ctx* ctx, double* c, double* pinv, double* u,
@@ -326,10 +332,11 @@ int sf_set_grid(sf_ctx* ctx, const double* x, int nx, const double* y,
   SF_REQUIRE((int64_t)nx * ny <= ((int64_t)1 << 31), SF_EINVAL,
              "sf_set_grid: grid too large");
   SF_HIP(hipSetDevice(ctx->device));
+  ctx->n_pix = 0;  // no usable grid until the pixel basis is built
   ctx->nx = nx;
   ctx->ny = ny;
-  ctx->n_pix = (int64_t)nx * ny;
-  ctx->n_pix_blocks = (ctx->n_pix + sf::kBlockPix - 1) / sf::kBlockPix;
+  const int64_t n_pix = (int64_t)nx * ny;
+  ctx->n_pix_blocks = (n_pix + sf::kBlockPix - 1) / sf::kBlockPix;
   ctx->ksteps = (ctx->D + 3) / 4;
   const size_t n = (size_t)ctx->n_pix_blocks * sf::kEvalWaves * ctx->ksteps *
                    sf::kTiles * 64;
@@ -342,12 +349,22 @@ int sf_set_grid(sf_ctx* ctx, const double* x, int nx, const double* y,
     hipFree(dx);
     return rc;
   }
-  hipMemcpyAsync(dx, x, sizeof(double) * nx, hipMemcpyHostToDevice, ctx->stream);
-  hipMemcpyAsync(dy, y, sizeof(double) * ny, hipMemcpyHostToDevice, ctx->stream);
-  rc = sf::launch_cpix(ctx, dx, dy);
-  hipStreamSynchronize(ctx->stream);
-  hipFree(dx);
-  hipFree(dy);
+  if (hipMemcpyAsync(dx, x, sizeof(double) * nx, hipMemcpyHostToDevice,
+                     ctx->stream) != hipSuccess ||
+      hipMemcpyAsync(dy, y, sizeof(double) * ny, hipMemcpyHostToDevice,
+                     ctx->stream) != hipSuccess) {
+    set_error("sf_set_grid: copy of the grid coordinates failed");
+    rc = SF_EIO;
+  } else {
+    rc = sf::launch_cpix(ctx, dx, dy);
+  }
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess && rc == SF_OK) {
+    set_error("sf_set_grid: pixel basis kernel failed");
+    rc = SF_EIO;
+  }
+  (void)hipFree(dx);
+  (void)hipFree(dy);
+  if (rc == SF_OK) ctx->n_pix = n_pix;
   return rc;
 }
 

@@ -689,8 +689,14 @@ int grow(T** p, size_t& cap, size_t need, bool keep = false) {
     set_error("hipMalloc failed (fit scratch)");
     return SF_ENOMEM;
   }
-  if (keep && *p && cap > 0)
-    hipMemcpy(q, *p, cap * sizeof(T), hipMemcpyDeviceToDevice);
+  // callers synchronise the context stream before growing, so the old
+  // buffer is no longer written by queued kernels
+  if (keep && *p && cap > 0 &&
+      hipMemcpy(q, *p, cap * sizeof(T), hipMemcpyDeviceToDevice) != hipSuccess) {
+    (void)hipFree(q);
+    set_error("hipMemcpy failed (fit scratch grow)");
+    return SF_EIO;
+  }
   if (*p) (void)hipFree(*p);
   *p = q;
   cap = need;

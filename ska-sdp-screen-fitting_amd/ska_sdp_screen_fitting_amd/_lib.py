@@ -125,19 +125,28 @@ def _check(rc, what):
         raise ScreenFitError(f"{what} failed ({rc}): {msg}")
 
 
-def _ptr(x):
-    """Device/host pointer of a torch tensor, numpy array or int."""
-    if x is None:
-        return None
-    if isinstance(x, int):
+_TORCH_DTYPES = {np.float64: "torch.float64", np.float32: "torch.float32",
+                 np.int32: "torch.int32"}
+
+
+def _dev(x, dtype, numel, name):
+    """Pointer of a device operand after checking what the kernels assume:
+    a contiguous CUDA tensor of ``dtype`` with at least ``numel`` elements
+    (a short or mistyped buffer would be overrun on the GPU).  Raw integer
+    pointers are the caller's responsibility."""
+    if x is None or isinstance(x, int):
         return x
-    if isinstance(x, np.ndarray):
-        assert x.flags["C_CONTIGUOUS"], "arrays passed to the C ABI must be contiguous"
-        return x.ctypes.data
-    if hasattr(x, "data_ptr"):
-        assert x.is_contiguous(), "tensors passed to the C ABI must be contiguous"
-        return x.data_ptr()
-    raise TypeError(type(x))
+    if not hasattr(x, "data_ptr"):
+        raise TypeError(f"{name}: expected a device tensor, got {type(x).__name__}")
+    if not x.is_cuda:
+        raise ValueError(f"{name}: must be a device (cuda) tensor")
+    if str(x.dtype) != _TORCH_DTYPES[dtype]:
+        raise TypeError(f"{name}: dtype {x.dtype}, expected {_TORCH_DTYPES[dtype]}")
+    if not x.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    if x.numel() < numel:
+        raise ValueError(f"{name}: {x.numel()} elements, the call needs {numel}")
+    return x.data_ptr()
 
 
 class Context:
@@ -203,15 +212,22 @@ class Context:
             ref_phase=None):
         """sf_kl_fit on device buffers (torch tensors or raw pointers)."""
         so = np.ascontiguousarray(station_order, dtype=np.int32)
-        assert so.shape == (A,)
+        if so.shape != (A,):
+            raise ValueError(f"station_order: shape {so.shape}, expected ({A},)")
+        n = int(T) * int(F) * int(A) * self.D
         prm = FitParams(int(screen_type), int(niter), float(nsigma),
                         int(bool(adjust_order)), int(ref_ant), int(ant_offset),
-                        _ptr(ref_phase))
+                        _dev(ref_phase, np.float64, int(T) * int(F) * self.D,
+                             "ref_phase"))
         _check(self.lib.sf_kl_fit(
-            self.h, _ptr(phase), _ptr(weight), int(T), int(F), int(A),
+            self.h, _dev(phase, np.float64, n, "phase"),
+            _dev(weight, np.float32, n, "weight"), int(T), int(F), int(A),
             so.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
-            ctypes.byref(prm), _ptr(coef), _ptr(resid), _ptr(w_out),
-            _ptr(order_out)), "sf_kl_fit")
+            ctypes.byref(prm), _dev(coef, np.float64, n, "coef"),
+            _dev(resid, np.float64, n, "resid"),
+            _dev(w_out, np.float32, n, "w_out"),
+            _dev(order_out, np.int32, n // max(self.D, 1), "order_out")),
+            "sf_kl_fit")
 
     def fit_stats(self):
         nm, ng = ctypes.c_int(), ctypes.c_int()
@@ -226,11 +242,17 @@ class Context:
                                     y.ctypes.data, y.size), "sf_set_grid")
         self.grid = (x.size, y.size)
 
+    def _out_numel(self, S, ring):
+        nx, ny = self.grid if self.grid else (0, 0)
+        return min(int(S), ring) * 4 * nx * ny
+
     def eval(self, coef, S, out, ring_slots=None,
              flags=SF_EVAL_NAN_SCRUB | SF_EVAL_FAST_SINCOS | SF_EVAL_NT_STORES):
-        ring = int(S if ring_slots is None else ring_slots)
-        _check(self.lib.sf_kl_eval(self.h, _ptr(coef), int(S), _ptr(out),
-                                   max(ring, 1), int(flags)), "sf_kl_eval")
+        ring = max(int(S if ring_slots is None else ring_slots), 1)
+        _check(self.lib.sf_kl_eval(
+            self.h, _dev(coef, np.float64, int(S) * self.D, "coef"), int(S),
+            _dev(out, np.float32, self._out_numel(S, ring), "out"), ring,
+            int(flags)), "sf_kl_eval")
 
 
     def device_cus(self):
@@ -253,21 +275,27 @@ class Context:
 
     def eval_gain(self, coef_ph, coef_xx, coef_yy, S, out, ring_slots=None,
                   flags=SF_EVAL_NAN_SCRUB | SF_EVAL_FAST_SINCOS | SF_EVAL_NT_STORES):
-        ring = int(S if ring_slots is None else ring_slots)
-        _check(self.lib.sf_kl_eval_gain(self.h, _ptr(coef_ph), _ptr(coef_xx),
-                                        _ptr(coef_yy), int(S), _ptr(out),
-                                        max(ring, 1), int(flags)),
-               "sf_kl_eval_gain")
+        ring = max(int(S if ring_slots is None else ring_slots), 1)
+        n = int(S) * self.D
+        _check(self.lib.sf_kl_eval_gain(
+            self.h, _dev(coef_ph, np.float64, n, "coef_ph"),
+            _dev(coef_xx, np.float64, n, "coef_xx"),
+            _dev(coef_yy, np.float64, n, "coef_yy"), int(S),
+            _dev(out, np.float32, self._out_numel(S, ring), "out"), ring,
+            int(flags)), "sf_kl_eval_gain")
 
     def tess_fill(self, labels, nx, ny, phase, D, S, out, ring_slots=None,
                   amp_xx=None, amp_yy=None, smooth_pix=0.0,
                   flags=SF_EVAL_NAN_SCRUB):
-        ring = int(S if ring_slots is None else ring_slots)
-        _check(self.lib.sf_tess_fill(self.h, _ptr(labels), int(nx), int(ny),
-                                     _ptr(phase), _ptr(amp_xx), _ptr(amp_yy),
-                                     int(D), int(S), _ptr(out), max(ring, 1),
-                                     float(smooth_pix), int(flags)),
-               "sf_tess_fill")
+        ring = max(int(S if ring_slots is None else ring_slots), 1)
+        n = int(S) * int(D)
+        _check(self.lib.sf_tess_fill(
+            self.h, _dev(labels, np.int32, int(nx) * int(ny), "labels"),
+            int(nx), int(ny), _dev(phase, np.float64, n, "phase"),
+            _dev(amp_xx, np.float64, n, "amp_xx"),
+            _dev(amp_yy, np.float64, n, "amp_yy"), int(D), int(S),
+            _dev(out, np.float32, min(int(S), ring) * 4 * int(nx) * int(ny), "out"),
+            ring, float(smooth_pix), int(flags)), "sf_tess_fill")
 
 
 _contexts = {}

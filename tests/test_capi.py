@@ -63,3 +63,17 @@ def test_missing_library_fails_loudly(tmp_path):
     from ska_sdp_screen_fitting_amd._lib import ScreenFitError, load_library
     with pytest.raises(ScreenFitError):
         load_library(str(tmp_path / "nope.so"))
+
+
+def test_device_operands_are_checked_on_the_host():
+    """Host-side operand checks of the Python binding (no GPU needed for
+    these paths): host arrays and CPU tensors never reach a kernel."""
+    import numpy as np
+    from ska_sdp_screen_fitting_amd._lib import _dev
+    torch = pytest.importorskip("torch")
+    with pytest.raises(TypeError):
+        _dev(np.zeros(4), np.float64, 4, "coef")
+    with pytest.raises(ValueError):
+        _dev(torch.zeros(4, dtype=torch.float64), np.float64, 4, "coef")
+    assert _dev(None, np.float64, 4, "resid") is None
+    assert _dev(1234, np.float64, 4, "raw") == 1234

@@ -335,3 +335,23 @@ def test_eval_kernels_agree(ctx, dev, n_dir, grid):
     good = np.isfinite(coef).all(axis=1)
     want = okl.eval_planes(okl.eval_phase_screens(coef[good], cpix))
     np.testing.assert_allclose(ref[good].reshape(want.shape), want, rtol=0, atol=2e-6)
+
+
+def test_binding_rejects_bad_device_operands(ctx, dev):
+    """Wrong dtype / short / strided device buffers raise before any launch."""
+    pp = np.stack([np.linspace(-900, 900, 6), np.linspace(300, -300, 6), np.zeros(6)], 1)
+    ctx.set_basis(pp)
+    x = np.linspace(-500, 500, 16)
+    ctx.set_grid(x, x)
+    S = 5
+    coef = torch.zeros((S, 6), dtype=torch.float64, device=dev)
+    out = torch.empty((S, 4, 16, 16), dtype=torch.float32, device=dev)
+    with pytest.raises(TypeError):
+        ctx.eval(coef.float(), S, out)
+    with pytest.raises(ValueError):
+        ctx.eval(coef, S, out[: S - 1])
+    with pytest.raises(ValueError):
+        ctx.eval(coef[:, ::2], S, out)
+    ctx.eval(coef, S, out)  # the well-formed call still works
+    torch.cuda.synchronize()
+    assert torch.all(out[:, 0] == 1.0)
