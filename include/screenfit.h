@@ -113,6 +113,9 @@ int sf_device_cus(sf_ctx* ctx, int* n_cu);
  * the dispatch limit); each workgroup then walks several (pixel block, slot
  * chunk) items.  For tests of that walk. */
 #define SF_OPT_EVAL_MAX_BLOCKS 3
+/* SF_OPT_FIT_PACK = 0 runs one slot per wavefront in the fit also for
+ * D <= 32 (default 1: two slots per wavefront; same results bit for bit). */
+#define SF_OPT_FIT_PACK 4
 #define SF_EVAL_KERNEL_AUTO 0
 #define SF_EVAL_KERNEL_TILE 1
 #define SF_EVAL_KERNEL_LDS4 2

@@ -160,6 +160,9 @@ int sf_set_option(sf_ctx* ctx, int option, int value) {
                  SF_EINVAL, "sf_set_option: unknown evaluation kernel");
       ctx->eval_kernel = value;
       return SF_OK;
+    case SF_OPT_FIT_PACK:
+      ctx->fit_pack = value != 0;
+      return SF_OK;
     case SF_OPT_EVAL_MAX_BLOCKS:
       SF_REQUIRE(value >= 0, SF_EINVAL, "sf_set_option: negative block cap");
       ctx->eval_max_blocks = value;

@@ -217,13 +217,14 @@ __device__ __forceinline__ double model_value(int screen_type, double x) {
 // One _fit_screen (stationscreen.py:433-594) in the eigenbasis.  Lanes p < n
 // carry the unflagged directions (phi_p, w_p); returns, per DIRECTION lane d,
 // white_d and resid_d.
-template <bool SLOW>
+template <bool SLOW, int SPW>
 __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
                          int K, int screen_type, bool uniform, double wu,
                          double phi_p, double w_p, double phi_d, double w_d,
                          double& white_d, double& resid_d) {
 #pragma clang fp contract(off)
-  const int l = lane();
+  using G = Group<SPW>;
+  const int l = G::lane();
   const int n = B.n;
   double* v0 = L.vec;
   double* v1 = L.vec + 64;
@@ -270,7 +271,7 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
       }
       lds_sync();
       if (!SLOW) {
-        wave_cholesky_solve2(L.G, K, ld, a1, a2);
+        wave_cholesky_solve2<SPW>(L.G, K, ld, a1, a2);
       } else {
         // pinv(G, atol=1e-3) = sum_{|mu| > 1e-3} z z^T / mu (scipy >= 1.7)
         wave_jacobi(L.G, L.M, L.cs, L.pr, K, ld, 40);
@@ -361,12 +362,11 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
   }
   lds_sync();
   const bool unfl = (l < D) && (w_d > 0.0);
-  const unsigned long long m = __ballot(unfl);
+  const unsigned long long m = G::ballot(unfl);
   double sall = 0.0;
   if (l < D) {
     if (unfl) {
-      const int p = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+      const int p = G::rank(m);
       sall = v0[p];
     } else {
       // C[l][idx p]: idx p = p-th set bit of m
@@ -407,7 +407,7 @@ __device__ __forceinline__ double screen_diff(int screen_type, double val,
   return resid;
 }
 
-template <bool SLOW>
+template <bool SLOW, int SPW>
 __global__ __launch_bounds__(256) void kl_fit_pass_kernel(
     int it, int niter, int64_t S, int F, int A, int D,
     const double* __restrict__ phase, const double* __restrict__ refph,
@@ -422,9 +422,11 @@ __global__ __launch_bounds__(256) void kl_fit_pass_kernel(
 #pragma clang fp contract(off)
   extern __shared__ double smem[];
   const int ld = ldo(D);
+  using G = Group<SPW>;
   const int nwaves = blockDim.x / 64;
-  const int wv = threadIdx.x / 64;
-  const int d = lane();
+  const int nslots = nwaves * SPW;                  // slots in flight per WG
+  const int wv = (threadIdx.x / 64) * SPW + G::index();  // slot of the WG
+  const int d = G::lane();
   double* sU = smem;
   double* sC = sU + D * ld;
   double* sl = sC + D * ld;
@@ -449,8 +451,8 @@ __global__ __launch_bounds__(256) void kl_fit_pass_kernel(
   L.pr = reinterpret_cast<int2*>(L.cs + 64);
   const uint8_t want = SLOW ? 2 : 0;
 
-  for (int64_t s = (int64_t)blockIdx.x * nwaves + wv; s < S;
-       s += (int64_t)gridDim.x * nwaves) {
+  for (int64_t s = (int64_t)blockIdx.x * nslots + wv; s < S;
+       s += (int64_t)gridDim.x * nslots) {
     if (cls[s] != want) continue;
     const int a = (int)(s % A);
     const int p0 = pos[s];
@@ -476,7 +478,7 @@ __global__ __launch_bounds__(256) void kl_fit_pass_kernel(
     double order = (double)order_out[s];
     const double station_order = (double)st_order[a];
     const bool unfl = (d < D) && (w_d > 0.0);
-    const unsigned long long um = __ballot(unfl);
+    const unsigned long long um = G::ballot(unfl);
     const int n_unfl = __popcll(um);
 
     Basis B;
@@ -500,8 +502,7 @@ __global__ __launch_bounds__(256) void kl_fit_pass_kernel(
       double* v4 = L.vec + 256;
       double* v5 = L.vec + 320;
       if (unfl) {
-        const int p = __builtin_amdgcn_mbcnt_hi((uint32_t)(um >> 32),
-                                                __builtin_amdgcn_mbcnt_lo((uint32_t)um, 0));
+        const int p = G::rank(um);
         v4[p] = phi_d;
         v5[p] = w_d;
       }
@@ -512,14 +513,14 @@ __global__ __launch_bounds__(256) void kl_fit_pass_kernel(
       }
       lds_sync();
     }
-    const double wmax = wave_max(unfl ? w_d : -INFINITY);
-    const double wmin = -wave_max(unfl ? -w_d : -INFINITY);
+    const double wmax = G::max(unfl ? w_d : -INFINITY);
+    const double wmin = -G::max(unfl ? -w_d : -INFINITY);
     const bool uniform = (wmax == wmin);
 
     if (n_unfl > 0) {
       if (order > n_unfl - 1) order = n_unfl - 1;
       if (it == 0) {
-        fit_once<SLOW>(L, B, D, ld, (int)order, screen_type, uniform, wmin,
+        fit_once<SLOW, SPW>(L, B, D, ld, (int)order, screen_type, uniform, wmin,
                        phi_p, w_p, phi_d, w_d, white_d, resid_d);
       } else if (adjust_order) {
         bool hit_upper = false, hit_lower = false, hit_upper2 = false,
@@ -528,7 +529,7 @@ __global__ __launch_bounds__(256) void kl_fit_pass_kernel(
         for (int oi = 0; oi < 4; ++oi) {
           // oi == 0: the weights always compare equal (quirk Q2) -> no fit
           if (oi > 0)
-            fit_once<SLOW>(L, B, D, ld, (int)order, screen_type, uniform, wmin,
+            fit_once<SLOW, SPW>(L, B, D, ld, (int)order, screen_type, uniform, wmin,
                            phi_p, w_p, phi_d, w_d, white_d, resid_d);
           if (hit_lower2 || hit_upper2) break;
           double redchi2;
@@ -536,9 +537,9 @@ __global__ __launch_bounds__(256) void kl_fit_pass_kernel(
             double sn = 0.0, cn = 0.0;
             if (unfl) sincos(resid_d, &sn, &cn);
             const double ww = unfl ? w_d : 0.0;
-            const double sw = wave_sum(ww);
-            const double m1 = wave_sum(sn * sn * ww) / sw;
-            const double m2 = wave_sum(cn * cn * ww) / sw;
+            const double sw = G::sum(ww);
+            const double m1 = G::sum(sn * sn * ww) / sw;
+            const double m2 = G::sum(cn * cn * ww) / sw;
             redchi2 = (1.0 - hypot(m1, m2)) * sw / (n_unfl - order);
           } else {
             // np.sum(square(diff) * w) over all directions
@@ -547,7 +548,7 @@ __global__ __launch_bounds__(256) void kl_fit_pass_kernel(
               const double sd = screen_diff(screen_type, phi_d, resid_d);
               t = (sd * sd) * w_d;
             }
-            redchi2 = wave_sum(t) / (n_unfl - order);
+            redchi2 = G::sum(t) / (n_unfl - order);
           }
           if (oi > 0) {
             if (redchi2 > 1.0 && prev_redchi2 < redchi2) sign = -sign;
@@ -577,21 +578,21 @@ __global__ __launch_bounds__(256) void kl_fit_pass_kernel(
     // tec / amplitude: one sigma per station block -> kl_block_sigma/flag
     if (it + 1 < niter && screen_type == SF_SCREEN_PHASE) {
       const bool live = d < D;
-      if (__any(live && w_d > 0.0)) {
+      if (G::any(live && w_d > 0.0)) {
         double r = fmod(resid_d, 2.0 * M_PI);
         if (r < -M_PI) r += 2.0 * M_PI;
         if (r > M_PI) r -= 2.0 * M_PI;
         const bool inc = live && (w_d != 0.0) && !isnan(r);
         double sn = 0.0, cn = 0.0;
         if (inc) sincos(r, &sn, &cn);
-        const double cnt = wave_sum(inc ? 1.0 : 0.0);
-        const double ms = wave_sum(sn) / cnt;
-        const double mc = wave_sum(cn) / cnt;
+        const double cnt = G::sum(inc ? 1.0 : 0.0);
+        const double ms = G::sum(sn) / cnt;
+        const double mc = G::sum(cn) / cnt;
         const double stdv = sqrt(-2.0 * log(hypot(ms, mc)));
         const bool outl = live && (fabs(r) > nsigma * stdv);
         if (outl) w_d = 0.0;
-        if (__any(outl)) {
-          const unsigned long long nm = __ballot(live && w_d > 0.0);
+        if (G::any(outl)) {
+          const unsigned long long nm = G::ballot(live && w_d > 0.0);
           if (d == 0) pos[s] = (nm == 0ull) ? -2 : table_insert(keys, cap, nm);
         }
       }
@@ -787,20 +788,20 @@ static int number_and_decompose(sf_ctx* ctx, int* n_slow) {
   return SF_OK;
 }
 
-template <bool SLOW>
-static int launch_pass(sf_ctx* ctx, int it, const sf_fit_params* p,
-                       const RefSpec& r, int64_t S, int F, int A,
-                       const double* phase, double* coef, double* resid,
-                       float* w_out, int32_t* order_out) {
+template <bool SLOW, int SPW>
+static int launch_pass_spw(sf_ctx* ctx, int it, const sf_fit_params* p,
+                           const RefSpec& r, int64_t S, int F, int A,
+                           const double* phase, double* coef, double* resid,
+                           float* w_out, int32_t* order_out) {
   const int D = ctx->D;
   const size_t shared = fast_shared_bytes(D);
-  const size_t wave = fast_wave_bytes(D, SLOW);
+  const size_t slot = fast_wave_bytes(D, SLOW);  // per-slot LDS scratch
   // waves per workgroup (<= 4): the most resident waves per CU under the
-  // 160 KiB LDS of a gfx950 CU (the per-wave subset basis is D^2 doubles, so
-  // at D = 50 only 2 waves fit; the smaller workgroup wins ties)
+  // 160 KiB LDS of a gfx950 CU (the per-slot subset basis is D^2 doubles,
+  // so at D = 50 only 2 waves fit; the smaller workgroup wins ties)
   int nw = 1, best = 0;
   for (int k = 1; k <= 4; ++k) {
-    const size_t per_wg = shared + k * wave;
+    const size_t per_wg = shared + (size_t)k * SPW * slot;
     if (per_wg > kLdsBytes) break;
     const int waves = k * (int)(kLdsBytes / per_wg);
     if (waves > best) {
@@ -808,14 +809,14 @@ static int launch_pass(sf_ctx* ctx, int it, const sf_fit_params* p,
       nw = k;
     }
   }
-  const size_t shm = shared + nw * wave;
+  const size_t shm = shared + (size_t)nw * SPW * slot;
   if (shm > 64 * 1024)
     SF_HIP(hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&kl_fit_pass_kernel<SLOW>),
+        reinterpret_cast<const void*>(&kl_fit_pass_kernel<SLOW, SPW>),
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
-  int64_t blocks = (S + nw - 1) / nw;
+  int64_t blocks = (S + nw * SPW - 1) / (nw * SPW);
   if (blocks > 16384) blocks = 16384;
-  hipLaunchKernelGGL((kl_fit_pass_kernel<SLOW>), dim3((unsigned)blocks),
+  hipLaunchKernelGGL((kl_fit_pass_kernel<SLOW, SPW>), dim3((unsigned)blocks),
                      dim3(64 * nw), shm, ctx->stream, it, p->niter, S, F, A, D,
                      phase, r.refph, r.sub, ctx->d_u, ctx->d_c, ctx->d_eig,
                      ctx->d_st_order, ctx->d_class, ctx->d_pos, ctx->d_ids,
@@ -824,6 +825,21 @@ static int launch_pass(sf_ctx* ctx, int it, const sf_fit_params* p,
                      p->nsigma, p->adjust_order, coef, resid, w_out, order_out);
   SF_HIP(hipGetLastError());
   return SF_OK;
+}
+
+// The fast class packs two slots into one wavefront (two 32-lane groups)
+// while the directions fit in half a wave: D <= 20 leaves 44 of 64 lanes
+// idle otherwise, and the per-slot instruction stream is the fit's cost.
+template <bool SLOW>
+static int launch_pass(sf_ctx* ctx, int it, const sf_fit_params* p,
+                       const RefSpec& r, int64_t S, int F, int A,
+                       const double* phase, double* coef, double* resid,
+                       float* w_out, int32_t* order_out) {
+  if (!SLOW && ctx->D <= 32 && ctx->fit_pack)
+    return launch_pass_spw<SLOW, 2>(ctx, it, p, r, S, F, A, phase, coef, resid,
+                                    w_out, order_out);
+  return launch_pass_spw<SLOW, 1>(ctx, it, p, r, S, F, A, phase, coef, resid,
+                                  w_out, order_out);
 }
 
 int launch_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,

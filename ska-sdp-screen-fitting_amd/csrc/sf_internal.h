@@ -86,6 +86,7 @@ struct sf_ctx {
   // evaluation kernel (SF_OPT_EVAL_KERNEL)
   int eval_kernel = SF_EVAL_KERNEL_AUTO;
   int64_t eval_max_blocks = 0;  // SF_OPT_EVAL_MAX_BLOCKS (0 = dispatch limit)
+  int fit_pack = 1;             // SF_OPT_FIT_PACK: 2 slots per wave for D <= 32
 };
 
 namespace sf {

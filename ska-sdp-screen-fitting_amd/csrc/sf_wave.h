@@ -36,6 +36,46 @@ __device__ __forceinline__ double bcast(double v, int src) {
   return __shfl(v, src, 64);
 }
 
+// Lane group of one slot when a wavefront carries SPW independent slots
+// (SPW = 1: the whole wave; SPW = 2: two 32-lane halves, for D <= 32).
+// Every reduction / vote / broadcast stays inside the group, and with
+// SPW = 1 each is the exact 64-lane operation above (same order of adds),
+// so packing slots changes no result bit.
+template <int SPW>
+struct Group {
+  static constexpr int kWidth = 64 / SPW;
+  __device__ static int lane() { return __lane_id() & (kWidth - 1); }
+  __device__ static int first() { return __lane_id() & ~(kWidth - 1); }
+  __device__ static int index() { return __lane_id() / kWidth; }
+  __device__ static double sum(double v) {
+#pragma unroll
+    for (int o = kWidth / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+  }
+  __device__ static double max(double v) {
+#pragma unroll
+    for (int o = kWidth / 2; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    return v;
+  }
+  __device__ static double bcast(double v, int src) {
+    return __shfl(v, first() + src, 64);
+  }
+  // the group's vote bits, bit i = group lane i
+  __device__ static unsigned long long ballot(bool x) {
+    const unsigned long long m = __ballot(x);
+    if (SPW == 1) return m;
+    return (m >> first()) & ((1ull << kWidth) - 1);
+  }
+  __device__ static bool any(bool x) { return ballot(x) != 0ull; }
+  // number of set bits of the group mask m below this lane
+  __device__ static int rank(unsigned long long m) {
+    if (SPW == 1)
+      return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                       __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+    return __popcll(m & ((1ull << lane()) - 1));
+  }
+};
+
 // Round-robin (chess tournament) pairing of m = n + (n & 1) players over
 // m - 1 rounds; player m - 1 is fixed.  Returns the partner of i in round r
 // (a partner >= n means "sits out this round").
@@ -199,9 +239,11 @@ __device__ inline void wave_eig_order(const double* a, int n, int ld,
 // In-place Cholesky G = L L^T of the SPD k x k matrix g (lower triangle
 // used), then solves G x = b for two right-hand sides held one element per
 // lane (b1, b2 on lanes < k).  Returns the solutions in the same layout.
+template <int SPW = 1>
 __device__ inline void wave_cholesky_solve2(double* g, int k, int ld,
                                             double& b1, double& b2) {
-  const int i = lane();
+  using G = Group<SPW>;
+  const int i = G::lane();
   for (int c = 0; c < k; ++c) {
     const double piv = sqrt(g[c * ld + c]);
     lds_sync();
@@ -220,8 +262,8 @@ __device__ inline void wave_cholesky_solve2(double* g, int k, int ld,
   // forward: L y = b
   for (int c = 0; c < k; ++c) {
     const double lcc = g[c * ld + c];
-    const double y1 = bcast(b1, c) / lcc;
-    const double y2 = bcast(b2, c) / lcc;
+    const double y1 = G::bcast(b1, c) / lcc;
+    const double y2 = G::bcast(b2, c) / lcc;
     if (i == c) { b1 = y1; b2 = y2; }
     if (i > c && i < k) {
       const double lic = g[i * ld + c];
@@ -232,8 +274,8 @@ __device__ inline void wave_cholesky_solve2(double* g, int k, int ld,
   // backward: L^T x = y
   for (int c = k - 1; c >= 0; --c) {
     const double lcc = g[c * ld + c];
-    const double x1 = bcast(b1, c) / lcc;
-    const double x2 = bcast(b2, c) / lcc;
+    const double x1 = G::bcast(b1, c) / lcc;
+    const double x2 = G::bcast(b2, c) / lcc;
     if (i == c) { b1 = x1; b2 = x2; }
     if (i < c) {
       const double lci = g[c * ld + i];

@@ -15,6 +15,7 @@ import torch
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "ska-sdp-screen-fitting_amd"))
 from ska_sdp_screen_fitting_amd import geometry, get_context  # noqa: E402
+from ska_sdp_screen_fitting_amd._lib import SF_OPT_FIT_PACK  # noqa: E402
 from ska_sdp_screen_fitting_amd.stationscreen import station_orders  # noqa: E402
 from ska_sdp_screen_fitting_amd.synthetic import make_solutions  # noqa: E402
 
@@ -38,18 +39,22 @@ for sh in shapes:
         ctx.fit(ph, wt, T, F, A, st, ref_ant=0, coef=coef, order_out=order,
                 w_out=w_out, adjust_order=True, niter=2)
 
-    run()
-    torch.cuda.synchronize()
-    ts = []
-    for _ in range(3):
-        t0 = time.perf_counter()
+    for pack in (1, 0):
+        ctx.set_option(SF_OPT_FIT_PACK, pack)
         run()
         torch.cuda.synchronize()
-        ts.append(time.perf_counter() - t0)
-    ms = float(np.median(ts)) * 1e3
-    h = hashlib.sha1()
-    for t in (coef, order, w_out):
-        h.update(t.cpu().numpy().tobytes())
-    S = T * F * A
-    print(f"D={D} S={S}: {ms:9.2f} ms  {S / ms * 1e3 / 1e6:7.2f} M slots/s  "
-          f"{ctx.fit_stats()}  digest {h.hexdigest()[:16]}", flush=True)
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            run()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        ms = float(np.median(ts)) * 1e3
+        h = hashlib.sha1()
+        for t in (coef, order, w_out):
+            h.update(t.cpu().numpy().tobytes())
+        S = T * F * A
+        print(f"D={D} S={S} pack={pack}: {ms:9.2f} ms  "
+              f"{S / ms * 1e3 / 1e6:7.2f} M slots/s  {ctx.fit_stats()}  "
+              f"digest {h.hexdigest()[:16]}", flush=True)
+    ctx.set_option(SF_OPT_FIT_PACK, 1)
