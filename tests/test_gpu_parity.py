@@ -112,6 +112,22 @@ def test_fit_fast_equals_general_path(ctx, dev, name):
     np.testing.assert_allclose(fast[0][keep], gen[0][keep], rtol=0, atol=1e-9)
 
 
+@pytest.mark.parametrize("name", ["synth20", "synth12tiny", "fixture_kl"])
+def test_fit_two_slots_per_wave_is_bit_identical(ctx, dev, name):
+    """Two slots per wavefront (D <= 32) must not change a single bit: the
+    group reductions add in the same order as the 64-lane ones."""
+    from ska_sdp_screen_fitting_amd._lib import SF_OPT_FIT_PACK
+    g = load_golden(name)
+    packed = gpu_fit(ctx, dev, g)
+    ctx.set_option(SF_OPT_FIT_PACK, 0)
+    try:
+        single = gpu_fit(ctx, dev, g)
+    finally:
+        ctx.set_option(SF_OPT_FIT_PACK, 1)
+    for a, b in zip(packed, single):
+        assert np.array_equal(a.view(np.uint8), b.view(np.uint8))
+
+
 def test_fit_vs_oracle_config3_shape(ctx, dev):
     """A larger config-3-shaped synthetic (flags, outliers, adapted orders)."""
     from ska_sdp_screen_fitting_amd import geometry
