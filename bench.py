@@ -67,9 +67,11 @@ def parse():
     ap.add_argument("--reserve-cus", type=int, default=16,
                     help="compute units the eval stream leaves to the fit "
                          "stream (pipelined mode)")
-    ap.add_argument("--fit-on-reserved", type=int, default=0,
+    ap.add_argument("--fit-on-reserved", type=int, default=-1,
                     help="1: confine the fit stream to the reserved CUs "
-                         "(pipelined mode)")
+                         "(pipelined mode); -1 (default): when D <= 32, where "
+                         "the fit of a chunk on the reserved CUs is shorter "
+                         "than the evaluation of the previous one")
     ap.add_argument("--fit-priority", type=int, default=1,
                     help="1: fit stream at high priority (pipelined mode)")
     ap.add_argument("--eval-only", action="store_true",
@@ -248,6 +250,10 @@ def main():
     masked_handle = fit_handle = None
     if n_chunks > 1:
         fit_stream = torch.cuda.Stream(dev, priority=-1 if args.fit_priority else 0)
+    # the first fit of a run has the chip to itself (nothing to overlap):
+    # it runs on an unrestricted stream even when later fits are confined
+    first_fit_stream = fit_stream
+    if n_chunks > 1:
         if args.reserve_cus > 0:
             n_cu = ctx.device_cus()
             step = max(1, n_cu // args.reserve_cus)
@@ -256,16 +262,19 @@ def main():
             reserved = [min(n_cu - 1, k * step + k % 8) for k in range(args.reserve_cus)]
             masked_handle = ctx.stream_create(reserved)
             stream = torch.cuda.ExternalStream(masked_handle, device=dev)
-            if args.fit_on_reserved:
+            on_reserved = args.fit_on_reserved
+            if on_reserved < 0:
+                on_reserved = 1 if D <= 32 else 0
+            if on_reserved:
                 keep = set(reserved)
                 fit_handle = ctx.stream_create([c for c in range(n_cu) if c not in keep])
                 fit_stream = torch.cuda.ExternalStream(fit_handle, device=dev)
 
     eval_kernel_name = ctx.eval_kernel(flags)
 
-    def fit(c):
+    def fit(c, fs):
         t0, t1 = bounds[c]
-        ctx.set_stream(fit_stream.cuda_stream)
+        ctx.set_stream(fs.cuda_stream)
         ctx.fit(phase[t0:t1], weight[t0:t1], t1 - t0, F, A, setup["st_order"],
                 niter=2, nsigma=5.0, adjust_order=True, ref_ant=setup["ref_ant"],
                 coef=coef[t0:t1], resid=resid[t0:t1], w_out=w_out[t0:t1],
@@ -290,16 +299,19 @@ def main():
 
         def issue_fit(i):
             k, c = items[i]
+            fs = first_fit_stream if i == 0 else fit_stream
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             if i >= n_chunks:
                 # coef[chunk c] is rewritten: wait for the previous step's
                 # eval of the same chunk (write-after-read across streams)
-                fit_stream.wait_event(eval_done[i - n_chunks])
-            e0.record(fit_stream)
+                fs.wait_event(eval_done[i - n_chunks])
+            if i > 0:
+                fs.wait_event(fit_done[i - 1][1])  # fits share the ctx scratch
+            e0.record(fs)
             if not args.eval_only:
-                fit(c)
-            e1.record(fit_stream)
+                fit(c, fs)
+            e1.record(fs)
             fit_done[i] = (e0, e1)
 
         issue_fit(0)
@@ -318,7 +330,7 @@ def main():
 
     if args.eval_only:
         for c in range(n_chunks):
-            fit(c)
+            fit(c, first_fit_stream)
     run_steps(args.warmup)
     torch.cuda.synchronize(dev)
 

@@ -116,6 +116,12 @@ int sf_device_cus(sf_ctx* ctx, int* n_cu);
 /* SF_OPT_FIT_PACK = 0 runs one slot per wavefront in the fit also for
  * D <= 32 (default 1: two slots per wavefront; same results bit for bit). */
 #define SF_OPT_FIT_PACK 4
+/* SF_OPT_EVAL_KS_PAD = n (0..3) runs the evaluation contraction with n extra
+ * all-zero k-steps of 4 directions (same values; tuning / diagnostics). */
+#define SF_OPT_EVAL_KS_PAD 5
+/* SF_OPT_EVAL_SLEEP = n: LDS-staged evaluation waves sleep n x 64 cycles
+ * after each 16-slot contraction (store-throttling experiments; default 0). */
+#define SF_OPT_EVAL_SLEEP 6
 #define SF_EVAL_KERNEL_AUTO 0
 #define SF_EVAL_KERNEL_TILE 1
 #define SF_EVAL_KERNEL_LDS4 2

@@ -163,6 +163,16 @@ int sf_set_option(sf_ctx* ctx, int option, int value) {
     case SF_OPT_FIT_PACK:
       ctx->fit_pack = value != 0;
       return SF_OK;
+    case SF_OPT_EVAL_KS_PAD:
+      SF_REQUIRE(value >= 0 && value <= 3, SF_EINVAL,
+                 "sf_set_option: k-step padding must be 0..3");
+      ctx->eval_ks_pad = value;
+      return SF_OK;
+    case SF_OPT_EVAL_SLEEP:
+      SF_REQUIRE(value >= 0 && value <= 1000, SF_EINVAL,
+                 "sf_set_option: eval sleep must be 0..1000");
+      ctx->eval_sleep = value;
+      return SF_OK;
     case SF_OPT_EVAL_MAX_BLOCKS:
       SF_REQUIRE(value >= 0, SF_EINVAL, "sf_set_option: negative block cap");
       ctx->eval_max_blocks = value;

@@ -306,7 +306,8 @@ template <int KS, int NW, int TPW, bool NT>
 __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
     const double* __restrict__ cfrag, const double* __restrict__ coef, int D,
     int ks_real, int64_t S, int64_t P, int64_t n_pb, int64_t n_sc,
-    int chunk_groups, float* __restrict__ out, int64_t ring, unsigned flags) {
+    int chunk_groups, float* __restrict__ out, int64_t ring, unsigned flags,
+    int sleep) {
   using L = EvalLds<NW, TPW>;
   __shared__ float tile[2][16][L::kStride];
   const int l = threadIdx.x & 63;
@@ -374,6 +375,7 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
         else
           *reinterpret_cast<v2f*>(dst) = v2f{red[0], red[1 % TPW]};
       }
+      for (int z = 0; z < sleep; ++z) __builtin_amdgcn_s_sleep(1);
       __syncthreads();
       // ---- stores: wave w owns kSlotsPerWave slots of the group
 #pragma unroll
@@ -500,11 +502,13 @@ static int launch_eval_lds(sf_ctx* ctx, const double* coef, int64_t S,
   if (flags & SF_EVAL_NT_STORES)
     hipLaunchKernelGGL((kl_eval_lds_kernel<KS, NW, TPW, true>), dim3((unsigned)nblk),
                        dim3(64 * NW), 0, ctx->stream, ctx->d_cfrag, coef, ctx->D,
-                       ctx->ksteps, S, P, n_pb, n_sc, groups, out, ring, flags);
+                       ctx->ksteps, S, P, n_pb, n_sc, groups, out, ring, flags,
+                       ctx->eval_sleep);
   else
     hipLaunchKernelGGL((kl_eval_lds_kernel<KS, NW, TPW, false>), dim3((unsigned)nblk),
                        dim3(64 * NW), 0, ctx->stream, ctx->d_cfrag, coef, ctx->D,
-                       ctx->ksteps, S, P, n_pb, n_sc, groups, out, ring, flags);
+                       ctx->ksteps, S, P, n_pb, n_sc, groups, out, ring, flags,
+                       ctx->eval_sleep);
   SF_HIP(hipGetLastError());
   return SF_OK;
 }
@@ -560,7 +564,14 @@ static int launch_eval_pick(sf_ctx* ctx, const double* coef, const double* cxx,
 int launch_eval(sf_ctx* ctx, const double* coef, const double* cxx,
                 const double* cyy, int64_t S, float* out, int64_t ring,
                 unsigned flags) {
-  switch (ctx->ksteps) {
+  // zero k-step padding (SF_OPT_EVAL_KS_PAD) only for the LDS-staged
+  // kernels, which take the real k-step count for their Cpix indexing
+  const int v = pick_eval_kernel(ctx, cxx != nullptr, flags,
+                                 (reinterpret_cast<uintptr_t>(out) & 15) == 0);
+  const bool lds = v != SF_EVAL_KERNEL_TILE && v != SF_EVAL_KERNEL_TILE3;
+  int ks = ctx->ksteps + (lds ? ctx->eval_ks_pad : 0);
+  if (ks > 15) ks = ctx->ksteps;
+  switch (ks) {
 #define SF_KS(k) \
   case k:        \
     return launch_eval_pick<k>(ctx, coef, cxx, cyy, S, out, ring, flags);

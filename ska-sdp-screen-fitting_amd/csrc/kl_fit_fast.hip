@@ -73,9 +73,12 @@ __device__ __forceinline__ double phase_ref(const double* phase,
 }
 
 // ---------------------------------------------------------------------------
-// 1. classify slots, initialise the per-slot state, insert initial masks
-//    (one thread per slot)
+// 1. classify slots, initialise the per-slot state, insert initial masks.
+//    A slot is a group of GW = pow2 >= D lanes (64 / GW slots per wavefront),
+//    lane d of the group handles direction d, so every load and store of the
+//    [S][D] arrays is contiguous across the wave.
 // ---------------------------------------------------------------------------
+template <int GW>
 __global__ __launch_bounds__(256) void kl_classify_kernel(
     const float* __restrict__ weight, int64_t S, int F, int A, int D,
     const int* __restrict__ st_order, const uint8_t* __restrict__ skip,
@@ -84,16 +87,29 @@ __global__ __launch_bounds__(256) void kl_classify_kernel(
     int* __restrict__ counters,
     double* __restrict__ coef, double* __restrict__ resid,
     float* __restrict__ w_out, int32_t* __restrict__ order_out) {
-  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= S) return;
-  const int a = (int)(s % A);
-  const int f = (int)((s / A) % F);
-  const float* w = weight + s * D;
-  for (int d = 0; d < D; ++d) {
+  constexpr int kPerWave = 64 / GW;
+  const int l = lane();
+  const int g = l / GW;   // slot group within the wave
+  const int d = l % GW;   // direction
+  const int64_t s = ((int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) *
+                        kPerWave + g;
+  const bool live = s < S && d < D;
+  float x = 0.0f;
+  if (live) {
+    x = weight[s * D + d];
     coef[s * D + d] = 0.0;
     resid[s * D + d] = 0.0;
-    w_out[s * D + d] = w[d];
+    w_out[s * D + d] = x;
   }
+  // the group's unflagged-direction bits and tiny-weight vote
+  const unsigned long long bm = __ballot(live && x > 0.0f);
+  const unsigned long long bt = __ballot(live && x > 0.0f && (double)x <= kTinyW);
+  const unsigned long long gmask = (GW == 64) ? ~0ull : ((1ull << GW) - 1ull);
+  const unsigned long long mask = (bm >> (g * GW)) & gmask;
+  const bool tiny = ((bt >> (g * GW)) & gmask) != 0ull;
+  if (d != 0 || s >= S) return;
+  const int a = (int)(s % A);
+  const int f = (int)((s / A) % F);
   if (a == ref_skip || skip[f * A + a]) {  // stationscreen.py:818-825
     cls[s] = 1;
     order_out[s] = 0;
@@ -101,13 +117,6 @@ __global__ __launch_bounds__(256) void kl_classify_kernel(
     return;
   }
   order_out[s] = st_order[a];
-  unsigned long long mask = 0ull;
-  bool tiny = false;
-  for (int d = 0; d < D; ++d) {
-    const float x = w[d];
-    if (x > 0.0f) mask |= 1ull << d;
-    tiny |= (x > 0.0f) && ((double)x <= kTinyW);
-  }
   if (tiny) atomicAdd(counters + 2, 1);
   cls[s] = tiny ? 2 : 0;
   const unsigned long long full = (D == 64) ? ~0ull : ((1ull << D) - 1ull);
@@ -916,12 +925,25 @@ int launch_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,
   SF_HIP(hipMemsetAsync(ctx->d_ids, 0xff, ctx->table_cap * sizeof(int), ctx->stream));
   SF_HIP(hipMemsetAsync(ctx->d_counters, 0, 4 * sizeof(int), ctx->stream));
 
-  hipLaunchKernelGGL(kl_classify_kernel, dim3((unsigned)((S + 255) / 256)),
-                     dim3(256), 0, ctx->stream, weight, S, F, A, D,
-                     ctx->d_st_order, ctx->d_skip, r.skip, ctx->d_keys, cap,
-                     ctx->d_pos, ctx->d_class, ctx->d_counters, coef, resid,
-                     w_out, order_out);
-  SF_HIP(hipGetLastError());
+  {
+    // lane groups of GW >= D lanes per slot, 4 waves per workgroup
+    const int gw = D <= 8 ? 8 : D <= 16 ? 16 : D <= 32 ? 32 : 64;
+    const int64_t per_block = 4 * (64 / gw);
+    const dim3 grid((unsigned)((S + per_block - 1) / per_block));
+#define SF_CLASSIFY(W)                                                          \
+  hipLaunchKernelGGL(kl_classify_kernel<W>, grid, dim3(256), 0, ctx->stream,    \
+                     weight, S, F, A, D, ctx->d_st_order, ctx->d_skip, r.skip,  \
+                     ctx->d_keys, cap, ctx->d_pos, ctx->d_class,               \
+                     ctx->d_counters, coef, resid, w_out, order_out)
+    switch (gw) {
+      case 8: SF_CLASSIFY(8); break;
+      case 16: SF_CLASSIFY(16); break;
+      case 32: SF_CLASSIFY(32); break;
+      default: SF_CLASSIFY(64); break;
+    }
+#undef SF_CLASSIFY
+    SF_HIP(hipGetLastError());
+  }
 
   const bool block_flags = p->screen_type != SF_SCREEN_PHASE;
   for (int it = 0; it < p->niter; ++it) {

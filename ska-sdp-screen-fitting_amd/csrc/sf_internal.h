@@ -86,6 +86,8 @@ struct sf_ctx {
   // evaluation kernel (SF_OPT_EVAL_KERNEL)
   int eval_kernel = SF_EVAL_KERNEL_AUTO;
   int64_t eval_max_blocks = 0;  // SF_OPT_EVAL_MAX_BLOCKS (0 = dispatch limit)
+  int eval_ks_pad = 0;          // SF_OPT_EVAL_KS_PAD: extra zero k-steps
+  int eval_sleep = 0;           // SF_OPT_EVAL_SLEEP: x 64 cycles per group
   int fit_pack = 1;             // SF_OPT_FIT_PACK: 2 slots per wave for D <= 32
 };
 

@@ -25,6 +25,8 @@ SF_OPT_FIT_GENERAL = 1
 SF_OPT_EVAL_KERNEL = 2
 SF_OPT_EVAL_MAX_BLOCKS = 3
 SF_OPT_FIT_PACK = 4
+SF_OPT_EVAL_KS_PAD = 5
+SF_OPT_EVAL_SLEEP = 6
 SF_EVAL_KERNEL_AUTO = 0
 SF_EVAL_KERNEL_TILE = 1
 SF_EVAL_KERNEL_LDS4 = 2

@@ -20,7 +20,8 @@ from ska_sdp_screen_fitting_amd._lib import (  # noqa: E402
     SF_EVAL_FAST_SINCOS, SF_EVAL_KERNEL_AUTO, SF_EVAL_KERNEL_LDS4,
     SF_EVAL_KERNEL_LDS8, SF_EVAL_KERNEL_LDS8H, SF_EVAL_KERNEL_LDS16,
     SF_EVAL_KERNEL_LDS16H, SF_EVAL_KERNEL_TILE, SF_EVAL_KERNEL_TILE3,
-    SF_EVAL_NAN_SCRUB, SF_EVAL_NT_STORES, SF_OPT_EVAL_KERNEL)
+    SF_EVAL_NAN_SCRUB, SF_EVAL_NT_STORES, SF_OPT_EVAL_KERNEL,
+    SF_OPT_EVAL_KS_PAD, SF_OPT_EVAL_SLEEP)
 
 KERNELS = {"auto": SF_EVAL_KERNEL_AUTO, "tile": SF_EVAL_KERNEL_TILE,
            "tile3": SF_EVAL_KERNEL_TILE3,
@@ -44,8 +45,25 @@ ctx.set_stream(stream.cuda_stream)
 base = SF_EVAL_NAN_SCRUB | SF_EVAL_FAST_SINCOS
 variants = {}
 for v in args.variants.split(","):
-    k, _, nt = v.partition("+")
-    variants[v] = (KERNELS[k], base | (SF_EVAL_NT_STORES if nt == "nt" else 0))
+    # kernel[+nt][+padN][+sleepN]
+    k, *mods = v.split("+")
+    fl, pad, sleep = base, 0, 0
+    for m in mods:
+        if m == "nt":
+            fl |= SF_EVAL_NT_STORES
+        elif m.startswith("pad"):
+            pad = int(m[3:])
+        elif m.startswith("sleep"):
+            sleep = int(m[5:])
+        else:
+            raise SystemExit(f"unknown variant modifier {m}")
+    variants[v] = (KERNELS[k], fl, pad, sleep)
+
+
+def use(kv, pad=0, sleep=0):
+    ctx.set_option(SF_OPT_EVAL_KERNEL, kv)
+    ctx.set_option(SF_OPT_EVAL_KS_PAD, pad)
+    ctx.set_option(SF_OPT_EVAL_SLEEP, sleep)
 
 ring_bytes = 16 * 2 ** 30
 out_flat = torch.empty(ring_bytes // 4, dtype=torch.float32, device=dev)
@@ -73,8 +91,8 @@ for D, N, S, pp, coef in shapes:
     cchk = coef[:Sc].clone()
     cchk[5, min(3, D - 1)] = float("nan")
     ref = None
-    for name, (kv, fl) in variants.items():
-        ctx.set_option(SF_OPT_EVAL_KERNEL, kv)
+    for name, (kv, fl, pad, sleep) in variants.items():
+        use(kv, pad, sleep)
         o = torch.full((Sc, 4, N, N), -7.0, dtype=torch.float32, device=dev)
         ctx.eval(cchk, Sc, o, Sc, fl)
         torch.cuda.synchronize()
@@ -92,10 +110,10 @@ for rep in range(args.reps):
         select(D, N, pp)
         ring = ring_bytes // (16 * N * N)
         out = out_flat[: ring * 4 * N * N].view(ring, 4, N, N)
-        ctx.set_option(SF_OPT_EVAL_KERNEL, SF_EVAL_KERNEL_AUTO)
+        use(SF_EVAL_KERNEL_AUTO)
         ctx.eval(coef, S, out, ring, base)  # untimed: re-warm after select()
-        for name, (kv, fl) in variants.items():
-            ctx.set_option(SF_OPT_EVAL_KERNEL, kv)
+        for name, (kv, fl, pad, sleep) in variants.items():
+            use(kv, pad, sleep)
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record(stream)
