@@ -74,6 +74,9 @@ def parse():
                          "than the evaluation of the previous one")
     ap.add_argument("--fit-priority", type=int, default=1,
                     help="1: fit stream at high priority (pipelined mode)")
+    ap.add_argument("--eval-xcd-map", type=int, default=-1,
+                    help="SF_OPT_EVAL_XCD_MAP: -1 auto (default), 0 contiguous "
+                         "pixel blocks per XCD, 1 interleaved")
     ap.add_argument("--eval-only", action="store_true",
                     help="time only sf_kl_eval (profiling)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),

@@ -122,6 +122,12 @@ int sf_device_cus(sf_ctx* ctx, int* n_cu);
 /* SF_OPT_EVAL_SLEEP = n: LDS-staged evaluation waves sleep n x 64 cycles
  * after each 16-slot contraction (store-throttling experiments; default 0). */
 #define SF_OPT_EVAL_SLEEP 6
+/* SF_OPT_EVAL_XCD_MAP: workgroup -> pixel-block map of the evaluation
+ * kernels.  0: XCD x (workgroups are dealt round-robin over the 8 XCDs)
+ * takes a contiguous eighth of the pixel blocks; 1: XCD x takes the pixel
+ * blocks pb = x (mod 8); -1 (default): 1 when an XCD's eighth is at most 8
+ * pixel blocks (256^2 with 4 KiB runs: +2-3 % measured), else 0. */
+#define SF_OPT_EVAL_XCD_MAP 7
 #define SF_EVAL_KERNEL_AUTO 0
 #define SF_EVAL_KERNEL_TILE 1
 #define SF_EVAL_KERNEL_LDS4 2

@@ -173,6 +173,11 @@ int sf_set_option(sf_ctx* ctx, int option, int value) {
                  "sf_set_option: eval sleep must be 0..1000");
       ctx->eval_sleep = value;
       return SF_OK;
+    case SF_OPT_EVAL_XCD_MAP:
+      SF_REQUIRE(value >= -1 && value <= 1, SF_EINVAL,
+                 "sf_set_option: XCD map must be -1, 0 or 1");
+      ctx->eval_xcd_map = value;
+      return SF_OK;
     case SF_OPT_EVAL_MAX_BLOCKS:
       SF_REQUIRE(value >= 0, SF_EINVAL, "sf_set_option: negative block cap");
       ctx->eval_max_blocks = value;

@@ -101,17 +101,23 @@ __device__ __forceinline__ void sincos_reduced(float r, float& s, float& c) {
 
 // Workgroup index -> (pixel block, slot chunk).  XCD-aware when the pixel
 // blocks divide by 8: consecutive workgroups go to the 8 XCDs round-robin,
-// so XCD x owns pixel blocks [x*per, (x+1)*per) and their Cpix slices stay
+// so XCD x owns pixel blocks [x*per, (x+1)*per) -- or, with the interleaved
+// map (SF_OPT_EVAL_XCD_MAP), pb = x (mod 8) -- and their Cpix slices stay
 // in its L2.  The eval kernels walk bb = blockIdx.x, += gridDim.x (a
 // multiple of 8, so a workgroup stays on its XCD's pixel blocks): one HSA
 // dispatch counts at most 2^32 work-items, which config 5 (16 M slots per
 // GPU at 512^2) would exceed with one workgroup per (pixel block, chunk).
+// Internal flag bit (never set by callers: sf_kl_eval masks it): XCD x takes
+// the pixel blocks pb = x (mod 8) instead of a contiguous eighth.
+constexpr unsigned kEvalXcdInterleave = 1u << 30;
+
 __device__ __forceinline__ void eval_block(int64_t bb, int64_t n_pb,
-                                           int64_t& pb, int64_t& sc) {
+                                           int64_t& pb, int64_t& sc,
+                                           unsigned flags) {
   if ((n_pb & 7) == 0) {
     const int64_t per = n_pb >> 3;
     const int64_t x = bb & 7, i = bb >> 3;
-    pb = x * per + (i % per);
+    pb = (flags & kEvalXcdInterleave) ? (i % per) * 8 + x : x * per + (i % per);
     sc = i / per;
   } else {
     pb = bb % n_pb;
@@ -167,7 +173,7 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
   const int64_t n_blocks = n_pb * n_sc;
   for (int64_t bb = blockIdx.x; bb < n_blocks; bb += gridDim.x) {
     int64_t pb, sc;
-    eval_block(bb, n_pb, pb, sc);
+    eval_block(bb, n_pb, pb, sc, flags);
     if (sc >= n_sc) continue;
     const int64_t wpb = pb * kEvalWaves + w;
     const int64_t p0 = wpb * kWavePix + (int64_t)(l & 15) * kTiles;
@@ -315,7 +321,7 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
   const int64_t n_blocks = n_pb * n_sc;
   for (int64_t bb = blockIdx.x; bb < n_blocks; bb += gridDim.x) {
     int64_t pb, sc;
-    eval_block(bb, n_pb, pb, sc);
+    eval_block(bb, n_pb, pb, sc, flags);
     if (sc >= n_sc) continue;  // uniform per workgroup
     const int wblk = w / L::kWavesPerBlock;         // 64-pixel block in the run
     const int t0 = (w % L::kWavesPerBlock) * TPW;   // first tile of this wave
@@ -499,6 +505,11 @@ static int launch_eval_lds(sf_ctx* ctx, const double* coef, int64_t S,
     groups >>= 1;
   const int64_t n_sc = (S + 16 * groups - 1) / (16 * groups);
   const int64_t nblk = eval_grid(ctx, n_pb, n_sc, 64 * NW);
+  // auto XCD map: interleave the pixel blocks over the XCDs when each XCD's
+  // contiguous eighth would be <= 8 blocks (measured: 256^2 at 4 KiB runs
+  // +2-3 %, 512^2 -3 %; profiles/round1e_eval_xcd_map.txt)
+  if (ctx->eval_xcd_map < 0 && (n_pb & 7) == 0 && n_pb / 8 <= 8)
+    flags |= kEvalXcdInterleave;
   if (flags & SF_EVAL_NT_STORES)
     hipLaunchKernelGGL((kl_eval_lds_kernel<KS, NW, TPW, true>), dim3((unsigned)nblk),
                        dim3(64 * NW), 0, ctx->stream, ctx->d_cfrag, coef, ctx->D,
@@ -570,6 +581,8 @@ int launch_eval(sf_ctx* ctx, const double* coef, const double* cxx,
                                  (reinterpret_cast<uintptr_t>(out) & 15) == 0);
   const bool lds = v != SF_EVAL_KERNEL_TILE && v != SF_EVAL_KERNEL_TILE3;
   int ks = ctx->ksteps + (lds ? ctx->eval_ks_pad : 0);
+  flags &= ~kEvalXcdInterleave;
+  if (ctx->eval_xcd_map > 0) flags |= kEvalXcdInterleave;
   if (ks > 15) ks = ctx->ksteps;
   switch (ks) {
 #define SF_KS(k) \

@@ -88,6 +88,7 @@ struct sf_ctx {
   int64_t eval_max_blocks = 0;  // SF_OPT_EVAL_MAX_BLOCKS (0 = dispatch limit)
   int eval_ks_pad = 0;          // SF_OPT_EVAL_KS_PAD: extra zero k-steps
   int eval_sleep = 0;           // SF_OPT_EVAL_SLEEP: x 64 cycles per group
+  int eval_xcd_map = -1;        // SF_OPT_EVAL_XCD_MAP (-1 = auto)
   int fit_pack = 1;             // SF_OPT_FIT_PACK: 2 slots per wave for D <= 32
 };
 

@@ -315,7 +315,8 @@ def test_eval_kernels_agree(ctx, dev, n_dir, grid):
     from ska_sdp_screen_fitting_amd._lib import (
         EVAL_KERNEL_NAMES, SF_EVAL_BIG_ENDIAN, SF_EVAL_FAST_SINCOS,
         SF_EVAL_KERNEL_AUTO, SF_EVAL_KERNEL_TILE, SF_EVAL_NT_STORES,
-        SF_OPT_EVAL_KERNEL, SF_OPT_EVAL_MAX_BLOCKS)
+        SF_OPT_EVAL_KERNEL, SF_OPT_EVAL_KS_PAD, SF_OPT_EVAL_MAX_BLOCKS,
+        SF_OPT_EVAL_XCD_MAP)
     from ska_sdp_screen_fitting_amd.synthetic import make_solutions
     s = make_solutions(n_ant=2, n_time=2, n_freq=1, n_dir=n_dir, seed=4)
     pp, mra, mdec = geometry.piercepoints(s.dir_radec)
@@ -340,9 +341,20 @@ def test_eval_kernels_agree(ctx, dev, n_dir, grid):
             ctx.set_option(SF_OPT_EVAL_MAX_BLOCKS, 8)
             outs[(kv, "walk")] = gpu_eval(ctx, dev, pp, x, y, coef, flags=base)
             ctx.set_option(SF_OPT_EVAL_MAX_BLOCKS, 0)
+            # both workgroup -> pixel-block maps over the XCDs
+            for xm in (0, 1):
+                ctx.set_option(SF_OPT_EVAL_XCD_MAP, xm)
+                outs[(kv, "xcd", xm)] = gpu_eval(ctx, dev, pp, x, y, coef, flags=base)
+            ctx.set_option(SF_OPT_EVAL_XCD_MAP, -1)
+            # zero k-step padding of the contraction
+            ctx.set_option(SF_OPT_EVAL_KS_PAD, 2)
+            outs[(kv, "pad")] = gpu_eval(ctx, dev, pp, x, y, coef, flags=base)
+            ctx.set_option(SF_OPT_EVAL_KS_PAD, 0)
     finally:
         ctx.set_option(SF_OPT_EVAL_KERNEL, SF_EVAL_KERNEL_AUTO)
         ctx.set_option(SF_OPT_EVAL_MAX_BLOCKS, 0)
+        ctx.set_option(SF_OPT_EVAL_XCD_MAP, -1)
+        ctx.set_option(SF_OPT_EVAL_KS_PAD, 0)
     ref = outs[(SF_EVAL_KERNEL_TILE, 0)]
     for k, o in outs.items():
         assert np.array_equal(o.view(np.int32), ref.view(np.int32)), k

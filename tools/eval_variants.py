@@ -21,7 +21,7 @@ from ska_sdp_screen_fitting_amd._lib import (  # noqa: E402
     SF_EVAL_KERNEL_LDS8, SF_EVAL_KERNEL_LDS8H, SF_EVAL_KERNEL_LDS16,
     SF_EVAL_KERNEL_LDS16H, SF_EVAL_KERNEL_TILE, SF_EVAL_KERNEL_TILE3,
     SF_EVAL_NAN_SCRUB, SF_EVAL_NT_STORES, SF_OPT_EVAL_KERNEL,
-    SF_OPT_EVAL_KS_PAD, SF_OPT_EVAL_SLEEP)
+    SF_OPT_EVAL_KS_PAD, SF_OPT_EVAL_SLEEP, SF_OPT_EVAL_XCD_MAP)
 
 KERNELS = {"auto": SF_EVAL_KERNEL_AUTO, "tile": SF_EVAL_KERNEL_TILE,
            "tile3": SF_EVAL_KERNEL_TILE3,
@@ -45,9 +45,9 @@ ctx.set_stream(stream.cuda_stream)
 base = SF_EVAL_NAN_SCRUB | SF_EVAL_FAST_SINCOS
 variants = {}
 for v in args.variants.split(","):
-    # kernel[+nt][+padN][+sleepN]
+    # kernel[+nt][+padN][+sleepN][+xi]
     k, *mods = v.split("+")
-    fl, pad, sleep = base, 0, 0
+    fl, pad, sleep, xi = base, 0, 0, 0
     for m in mods:
         if m == "nt":
             fl |= SF_EVAL_NT_STORES
@@ -55,15 +55,19 @@ for v in args.variants.split(","):
             pad = int(m[3:])
         elif m.startswith("sleep"):
             sleep = int(m[5:])
+        elif m == "xi":
+            xi = 1
         else:
             raise SystemExit(f"unknown variant modifier {m}")
-    variants[v] = (KERNELS[k], fl, pad, sleep)
+    variants[v] = (KERNELS[k], fl, (pad, sleep, xi))
 
 
-def use(kv, pad=0, sleep=0):
+def use(kv, opts=(0, 0, 0)):
+    pad, sleep, xi = opts
     ctx.set_option(SF_OPT_EVAL_KERNEL, kv)
     ctx.set_option(SF_OPT_EVAL_KS_PAD, pad)
     ctx.set_option(SF_OPT_EVAL_SLEEP, sleep)
+    ctx.set_option(SF_OPT_EVAL_XCD_MAP, xi)
 
 ring_bytes = 16 * 2 ** 30
 out_flat = torch.empty(ring_bytes // 4, dtype=torch.float32, device=dev)
@@ -91,8 +95,8 @@ for D, N, S, pp, coef in shapes:
     cchk = coef[:Sc].clone()
     cchk[5, min(3, D - 1)] = float("nan")
     ref = None
-    for name, (kv, fl, pad, sleep) in variants.items():
-        use(kv, pad, sleep)
+    for name, (kv, fl, opts) in variants.items():
+        use(kv, opts)
         o = torch.full((Sc, 4, N, N), -7.0, dtype=torch.float32, device=dev)
         ctx.eval(cchk, Sc, o, Sc, fl)
         torch.cuda.synchronize()
@@ -112,8 +116,8 @@ for rep in range(args.reps):
         out = out_flat[: ring * 4 * N * N].view(ring, 4, N, N)
         use(SF_EVAL_KERNEL_AUTO)
         ctx.eval(coef, S, out, ring, base)  # untimed: re-warm after select()
-        for name, (kv, fl, pad, sleep) in variants.items():
-            use(kv, pad, sleep)
+        for name, (kv, fl, opts) in variants.items():
+            use(kv, opts)
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record(stream)

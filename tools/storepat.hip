@@ -159,6 +159,20 @@ __global__ __launch_bounds__(256) void patP(float* out, long S) {
   }
 }
 
+// X: patC at 256 x 256 with the workgroup -> 4 KiB chunk map rotated by
+// SHIFT chunks (SHIFT 0 = patC): tests whether a workgroup's XCD (dealt
+// round-robin, g % 8) and the chunk's address matter for write bandwidth
+template <int NT, int SHIFT>
+__global__ __launch_bounds__(256) void patX(float* out, long n4) {
+  const long per_iter = 256L * 256;
+  const int g = (blockIdx.x + SHIFT) & 255;
+  for (long it = 0; it * per_iter < n4; ++it) {
+    const long i = it * per_iter + (long)g * 256 + threadIdx.x;
+    v4f v = {1.f, 2.f, 3.f, 4.f};
+    if (i < n4) st<NT>(out + 4 * i, v);
+  }
+}
+
 template <int NT>
 static void launch(int k, float* out, long S, size_t bytes) {
   const long n_pb = P / 256, n_sc = S / 256, n4 = (long)(bytes / 16);
@@ -182,6 +196,11 @@ static void launch(int k, float* out, long S, size_t bytes) {
       break;
     }
     case 15: hipLaunchKernelGGL(patC<NT>, dim3(256), dim3(256), 0, 0, out, n4); break;
+    case 26: hipLaunchKernelGGL((patX<NT, 0>), dim3(256), dim3(256), 0, 0, out, n4); break;
+    case 27: hipLaunchKernelGGL((patX<NT, 1>), dim3(256), dim3(256), 0, 0, out, n4); break;
+    case 28: hipLaunchKernelGGL((patX<NT, 4>), dim3(256), dim3(256), 0, 0, out, n4); break;
+    case 29: hipLaunchKernelGGL((patX<NT, 8>), dim3(256), dim3(256), 0, 0, out, n4); break;
+    case 30: hipLaunchKernelGGL((patX<NT, 64>), dim3(256), dim3(256), 0, 0, out, n4); break;
     case 20: hipLaunchKernelGGL((patP<NT, 0, 256>), dim3(P / 256), dim3(256), 0, 0, out, S); break;
     case 21: hipLaunchKernelGGL((patP<NT, 1, 256>), dim3(P / 256), dim3(256), 0, 0, out, S); break;
     case 22: hipLaunchKernelGGL((patP<NT, 2, 256>), dim3(P / 256), dim3(256), 0, 0, out, S); break;
@@ -217,16 +236,17 @@ int main() {
                          "C  grid-stride 256 x 1024",
                          "P  persistent 256 px, plane/wave", "P  persistent 256 px, 4 slots/wave",
                          "P  persistent 256 px, slot-major", "P  persistent 512 px, plane/wave",
-                         "P  persistent 512 px, slot-major", "P  persistent 1024 px, plane/wave"};
+                         "P  persistent 512 px, slot-major", "P  persistent 1024 px, plane/wave",
+                         "X  256x256 chunk shift 0", "X  256x256 chunk shift 1",
+                         "X  256x256 chunk shift 4", "X  256x256 chunk shift 8",
+                         "X  256x256 chunk shift 64"};
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   for (int nt = 0; nt <= 4; ++nt) {
-    for (int k = 0; k < 26; ++k) {
-      if (k >= 10 && k < 15) continue;
-      if (k >= 16 && k < 20) continue;
-      if (k < 5 || (k >= 5 && k < 10 && k != 6)) continue;
-      if (nt >= 2) continue;
+    for (int k = 0; k < 31; ++k) {
+      if (k != 2 && k != 15 && k < 26) continue;
+      if (nt >= 1) continue;
       float best = 1e9;
       for (int rep = 0; rep < 5; ++rep) {
         hipEventRecord(e0);
