@@ -77,6 +77,9 @@ def parse():
     ap.add_argument("--eval-xcd-map", type=int, default=-1,
                     help="SF_OPT_EVAL_XCD_MAP: -1 auto (default), 0 contiguous "
                          "pixel blocks per XCD, 1 interleaved")
+    ap.add_argument("--checksum", default="auto", choices=("auto", "on", "off"),
+                    help="per-slot output checksums (sf_kl_eval_sums); auto: on "
+                         "for config4 / config5, whose cubes are discarded")
     ap.add_argument("--eval-only", action="store_true",
                     help="time only sf_kl_eval (profiling)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
@@ -173,6 +176,47 @@ def fits_wallclock():
     return res
 
 
+def sampled_slots_check(ctx, torch, dev, setup, coef, N, flags, slot_sums,
+                        n_evals, fast):
+    """Parity of sampled slots of the timed run (not timed): slots 0, S/2 and
+    S-1 evaluated alone vs an fp64 torch restatement of kl_screen.py:444-449
+    (|d| <= 2e-6 with the fp32 sincos epilogue, 1e-6 with fp64), and -- in
+    checksum mode -- their cube checksums vs the per-slot sums the streamed
+    launches accumulated (n_evals identical evaluations of each slot)."""
+    D = coef.shape[1]
+    P = N * N
+    pp = torch.as_tensor(setup["piercepoints"], dtype=torch.float64, device=dev)
+    xs = torch.as_tensor(setup["x"], dtype=torch.float64, device=dev)
+    ys = torch.as_tensor(setup["y"], dtype=torch.float64, device=dev)
+    d2 = ((pp[:, 0][None, None, :] - xs[None, :, None]) ** 2
+          + (pp[:, 1][None, None, :] - ys[:, None, None]) ** 2) + pp[:, 2] ** 2
+    cpix = (-((d2 / 100.0 ** 2) ** (5.0 / 6.0)) / 2.0).reshape(P, D)
+    del d2
+    one = torch.empty((1, 4, N, N), dtype=torch.float32, device=dev)
+    S = coef.shape[0]
+    err, sums_ok, slots = 0.0, True, sorted({0, S // 2, S - 1})
+    for k in slots:
+        ctx.eval(coef[k:k + 1], 1, one, 1, flags)
+        torch.cuda.synchronize(dev)
+        ph = cpix @ coef[k]
+        c, s = torch.cos(ph), torch.sin(ph)
+        want = torch.stack([c, s, c, s])
+        got = one[0].reshape(4, P).double()
+        live = ~torch.isnan(ph)  # NaN pixels are scrubbed to 1 / 0
+        if bool(live.any()):
+            err = max(err, float((got - want)[:, live].abs().max()))
+        if slot_sums is not None:
+            h = int((one.view(torch.int32).to(torch.int64) & 0xFFFFFFFF).sum())
+            sums_ok &= (h * n_evals) % 2 ** 64 == int(slot_sums[k]) % 2 ** 64
+    tol = 2e-6 if fast else 1e-6
+    res = {"slots": slots, "max_abs_err_vs_fp64": err, "tol": tol,
+           "ok": err <= tol}
+    if slot_sums is not None:
+        res["checksums_match"] = bool(sums_ok)
+        res["ok"] = res["ok"] and bool(sums_ok)
+    return res
+
+
 def main():
     args = parse()
     import torch
@@ -197,7 +241,8 @@ def main():
     from ska_sdp_screen_fitting_amd import get_context
     from ska_sdp_screen_fitting_amd._lib import (SF_EVAL_FAST_SINCOS,
                                                  SF_EVAL_NAN_SCRUB,
-                                                 SF_EVAL_NT_STORES)
+                                                 SF_EVAL_NT_STORES,
+                                                 SF_OPT_EVAL_XCD_MAP)
     from ska_sdp_screen_fitting_amd.distributed import setup_shard
     from ska_sdp_screen_fitting_amd.synthetic import (FIELD_DEC_DEG,
                                                       FIELD_RA_DEG,
@@ -273,7 +318,13 @@ def main():
                 fit_handle = ctx.stream_create([c for c in range(n_cu) if c not in keep])
                 fit_stream = torch.cuda.ExternalStream(fit_handle, device=dev)
 
+    ctx.set_option(SF_OPT_EVAL_XCD_MAP, args.eval_xcd_map)
     eval_kernel_name = ctx.eval_kernel(flags)
+    # discard + checksum mode: the cubes go
+    # through the HBM ring and every slot's checksum is accumulated
+    checksum = args.checksum == "on" or (args.checksum == "auto"
+                                         and args.workload in ("config4", "config5"))
+    slot_sums = torch.zeros(S, dtype=torch.int64, device=dev) if checksum else None
 
     def fit(c, fs):
         t0, t1 = bounds[c]
@@ -287,7 +338,12 @@ def main():
     def evaluate(c):
         t0, t1 = bounds[c]
         ctx.set_stream(stream.cuda_stream)
-        ctx.eval(coef[t0:t1].reshape(-1, D), (t1 - t0) * F * A, out, ring, flags)
+        n = (t1 - t0) * F * A
+        if checksum:
+            ctx.eval_sums(coef[t0:t1].reshape(-1, D), n, out,
+                          slot_sums[t0 * F * A:t1 * F * A], ring, flags=flags)
+        else:
+            ctx.eval(coef[t0:t1].reshape(-1, D), n, out, ring, flags)
 
     # work items in issue order: every step fits and evaluates all chunks;
     # eval(c) waits for fit(c) (event), fit(c+1) is issued after eval(c) so
@@ -361,6 +417,9 @@ def main():
     # parity spot check (cheap invariants, not timed): cos^2 + sin^2 = 1
     chk = out[: min(ring, 64)].float()
     unit_err = float((chk[:, 0] ** 2 + chk[:, 1] ** 2 - 1).abs().max())
+    sampled = sampled_slots_check(ctx, torch, dev, setup, coef.reshape(-1, D), N,
+                                  flags, slot_sums, args.warmup + args.steps,
+                                  not args.precise_sincos)
 
     if rank == 0:
         algo_bytes = S * (16 * P + 8 * D)  # SURVEY.md §8(d), per step
@@ -416,11 +475,12 @@ def main():
                           "overlap": "fit(c+1) || eval(c), %d time chunks" % n_chunks
                           if n_chunks > 1 else "none"},
             "fit_stats": fit_stats,
-            "check": {"max_abs_cos2_plus_sin2_minus_1": unit_err},
+            "check": {"max_abs_cos2_plus_sin2_minus_1": unit_err,
+                      "sampled_slots": sampled},
         }
-        if not args.no_fits:
+        if not args.no_fits and world == 1:
             line["fits_wallclock"] = fits_wallclock()
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(
                 sol, setup, max(1, min(args.cpu_workers, os.cpu_count() or 1)))
         print(json.dumps(line), flush=True)

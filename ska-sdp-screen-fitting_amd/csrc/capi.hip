@@ -394,7 +394,8 @@ int sf_kl_eval(sf_ctx* ctx, const double* coef, int64_t S, float* out,
              "sf_kl_eval: bad argument");
   if (S == 0) return SF_OK;
   SF_HIP(hipSetDevice(ctx->device));
-  return sf::launch_eval(ctx, coef, nullptr, nullptr, S, out, ring, flags);
+  return sf::launch_eval(ctx, coef, nullptr, nullptr, S, out, ring, flags,
+                         nullptr);
 }
 
 int sf_kl_eval_gain(sf_ctx* ctx, const double* coef_phase,
@@ -406,7 +407,24 @@ int sf_kl_eval_gain(sf_ctx* ctx, const double* coef_phase,
              SF_EINVAL, "sf_kl_eval_gain: bad argument");
   if (S == 0) return SF_OK;
   SF_HIP(hipSetDevice(ctx->device));
-  return sf::launch_eval(ctx, coef_phase, coef_xx, coef_yy, S, out, ring, flags);
+  return sf::launch_eval(ctx, coef_phase, coef_xx, coef_yy, S, out, ring, flags,
+                         nullptr);
+}
+
+int sf_kl_eval_sums(sf_ctx* ctx, const double* coef_phase,
+                    const double* coef_xx, const double* coef_yy, int64_t S,
+                    float* out, int64_t ring, unsigned flags,
+                    uint64_t* slot_sums) {
+  SF_REQUIRE(ctx && ctx->n_pix > 0 && ctx->d_cfrag, SF_EINVAL,
+             "sf_kl_eval_sums: call sf_set_grid first");
+  SF_REQUIRE(coef_phase && out && slot_sums && S >= 0 && ring >= 1,
+             SF_EINVAL, "sf_kl_eval_sums: bad argument");
+  SF_REQUIRE((coef_xx == nullptr) == (coef_yy == nullptr), SF_EINVAL,
+             "sf_kl_eval_sums: give both amplitude coefficient sets or neither");
+  if (S == 0) return SF_OK;
+  SF_HIP(hipSetDevice(ctx->device));
+  return sf::launch_eval(ctx, coef_phase, coef_xx, coef_yy, S, out, ring, flags,
+                         reinterpret_cast<unsigned long long*>(slot_sums));
 }
 
 int sf_tess_fill(sf_ctx* ctx, const int32_t* labels, int nx, int ny,

@@ -148,6 +148,14 @@ __device__ __forceinline__ float bswapf(float x) {
   return __uint_as_float(__builtin_bswap32(__float_as_uint(x)));
 }
 
+// Per-slot output checksum (sf_kl_eval_sums): the sum, mod 2^64, of the
+// 32-bit words the slot's cube holds (as stored: after the NaN scrub and any
+// byte swap).  Integer adds commute, so the value does not depend on which
+// lanes / waves / workgroups contribute in which order.
+__device__ __forceinline__ unsigned long long fbits(float x) {
+  return (unsigned long long)__float_as_uint(x);
+}
+
 template <bool NT>
 __device__ __forceinline__ void store4(float* p, v4f v) {
   if (NT) __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(p));
@@ -166,7 +174,8 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
     const double* __restrict__ cfrag, const double* __restrict__ coef,
     const double* __restrict__ coef_xx, const double* __restrict__ coef_yy,
     int D, int64_t S, int64_t P, int64_t n_pb, int64_t n_sc, int chunk_groups,
-    float* __restrict__ out, int64_t ring, unsigned flags) {
+    float* __restrict__ out, int64_t ring, unsigned flags,
+    unsigned long long* __restrict__ sums) {
   const int l = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   // XCD-aware block -> (pixel block, slot chunk)
@@ -235,7 +244,7 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int64_t s = s0 + acc_row(l, r);
-        if (s >= S) continue;
+        if (s >= S) continue;  // uniform over the 16 lanes of a slot row
         // planes 0..3 = Re XX, Im XX, Re YY, Im YY
         float pv[4][kTiles];
 #pragma unroll
@@ -261,6 +270,7 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
           }
         }
         float* o = out + ((s % ring) * 4) * P + p0;
+        unsigned long long cs = 0ull;
         if (VEC4) {
           // P % 4 == 0: a lane's 4 pixels are all inside the grid or all out
           // (the last wave block of a grid that is not a multiple of 64)
@@ -269,6 +279,7 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
             for (int q = 0; q < 4; ++q) {
               const v4f v = {pv[q][0], pv[q][1], pv[q][2], pv[q][3]};
               store4<NT>(o + q * P, v);
+              if (sums) cs += (fbits(v[0]) + fbits(v[1])) + (fbits(v[2]) + fbits(v[3]));
             }
           }
         } else {
@@ -276,9 +287,18 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
           for (int t = 0; t < kTiles; ++t) {
             if (p0 + t < P) {
 #pragma unroll
-              for (int q = 0; q < 4; ++q) o[q * P + t] = pv[q][t];
+              for (int q = 0; q < 4; ++q) {
+                o[q * P + t] = pv[q][t];
+                if (sums) cs += fbits(pv[q][t]);
+              }
             }
           }
+        }
+        if (sums) {
+          // the 16 lanes of this slot row hold its 64 pixels of the wave
+#pragma unroll
+          for (int m = 1; m < 16; m <<= 1) cs += __shfl_xor(cs, m, 64);
+          if ((l & 15) == 0) atomicAdd(sums + s, cs);
         }
       }
     }
@@ -313,7 +333,7 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
     const double* __restrict__ cfrag, const double* __restrict__ coef, int D,
     int ks_real, int64_t S, int64_t P, int64_t n_pb, int64_t n_sc,
     int chunk_groups, float* __restrict__ out, int64_t ring, unsigned flags,
-    int sleep) {
+    int sleep, unsigned long long* __restrict__ sums) {
   using L = EvalLds<NW, TPW>;
   __shared__ float tile[2][16][L::kStride];
   const int l = threadIdx.x & 63;
@@ -419,6 +439,18 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
             }
           }
         }
+        if (sums) {
+          // planes 0 / 2 hold cos, 1 / 3 sin: every value is stored twice
+          unsigned long long cs = 0ull;
+#pragma unroll
+          for (int c = 0; c < L::kChunks; ++c)
+            if (pix0 + c * 256 + 4 * l < P)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) cs += 2ull * (fbits(cv[c][e]) + fbits(sv[c][e]));
+#pragma unroll
+          for (int m = 1; m < 64; m <<= 1) cs += __shfl_xor(cs, m, 64);
+          if (l == 0) atomicAdd(sums + s, cs);
+        }
       }
     }
     // the next workgroup item reuses the LDS tiles from buffer 0
@@ -454,7 +486,8 @@ int launch_cpix(sf_ctx* ctx, const double* d_x, const double* d_y) {
 template <int KS, int MINW>
 static int launch_eval_ks(sf_ctx* ctx, const double* coef,
                           const double* cxx, const double* cyy, int64_t S,
-                          float* out, int64_t ring, unsigned flags) {
+                          float* out, int64_t ring, unsigned flags,
+                          unsigned long long* sums) {
   const int64_t P = ctx->n_pix;
   const int64_t n_pb = ctx->n_pix_blocks;
   // slot chunk per workgroup: 16 groups of 16 slots (1 MiB of output at
@@ -471,7 +504,7 @@ static int launch_eval_ks(sf_ctx* ctx, const double* coef,
 #define SF_LAUNCH(V, F, N, G)                                                 \
   hipLaunchKernelGGL((kl_eval_kernel<KS, MINW, V, F, N, G>), dim3((unsigned)nblk),  \
                      dim3(256), 0, ctx->stream, ctx->d_cfrag, coef, cxx, cyy, \
-                     ctx->D, S, P, n_pb, n_sc, groups, out, ring, flags)
+                     ctx->D, S, P, n_pb, n_sc, groups, out, ring, flags, sums)
 #define SF_LAUNCH_G(V, F, N) \
   do {                       \
     if (gain)                \
@@ -496,7 +529,8 @@ static int launch_eval_ks(sf_ctx* ctx, const double* coef,
 
 template <int KS, int NW, int TPW>
 static int launch_eval_lds(sf_ctx* ctx, const double* coef, int64_t S,
-                           float* out, int64_t ring, unsigned flags) {
+                           float* out, int64_t ring, unsigned flags,
+                           unsigned long long* sums) {
   const int64_t P = ctx->n_pix;
   const int64_t run = EvalLds<NW, TPW>::kRun;
   const int64_t n_pb = (P + run - 1) / run;
@@ -514,12 +548,12 @@ static int launch_eval_lds(sf_ctx* ctx, const double* coef, int64_t S,
     hipLaunchKernelGGL((kl_eval_lds_kernel<KS, NW, TPW, true>), dim3((unsigned)nblk),
                        dim3(64 * NW), 0, ctx->stream, ctx->d_cfrag, coef, ctx->D,
                        ctx->ksteps, S, P, n_pb, n_sc, groups, out, ring, flags,
-                       ctx->eval_sleep);
+                       ctx->eval_sleep, sums);
   else
     hipLaunchKernelGGL((kl_eval_lds_kernel<KS, NW, TPW, false>), dim3((unsigned)nblk),
                        dim3(64 * NW), 0, ctx->stream, ctx->d_cfrag, coef, ctx->D,
                        ctx->ksteps, S, P, n_pb, n_sc, groups, out, ring, flags,
-                       ctx->eval_sleep);
+                       ctx->eval_sleep, sums);
   SF_HIP(hipGetLastError());
   return SF_OK;
 }
@@ -549,32 +583,33 @@ int pick_eval_kernel(const sf_ctx* ctx, bool gain, unsigned flags,
 template <int KS>
 static int launch_eval_pick(sf_ctx* ctx, const double* coef, const double* cxx,
                             const double* cyy, int64_t S, float* out,
-                            int64_t ring, unsigned flags) {
+                            int64_t ring, unsigned flags,
+                            unsigned long long* sums) {
   const int v = pick_eval_kernel(ctx, cxx != nullptr, flags,
                                  (reinterpret_cast<uintptr_t>(out) & 15) == 0);
   switch (v) {
     case SF_EVAL_KERNEL_LDS4:
-      return launch_eval_lds<KS, 4, 4>(ctx, coef, S, out, ring, flags);
+      return launch_eval_lds<KS, 4, 4>(ctx, coef, S, out, ring, flags, sums);
     case SF_EVAL_KERNEL_LDS8:
-      return launch_eval_lds<KS, 8, 4>(ctx, coef, S, out, ring, flags);
+      return launch_eval_lds<KS, 8, 4>(ctx, coef, S, out, ring, flags, sums);
     case SF_EVAL_KERNEL_LDS16:
-      return launch_eval_lds<KS, 16, 4>(ctx, coef, S, out, ring, flags);
+      return launch_eval_lds<KS, 16, 4>(ctx, coef, S, out, ring, flags, sums);
     case SF_EVAL_KERNEL_LDS8H:
-      return launch_eval_lds<KS, 8, 2>(ctx, coef, S, out, ring, flags);
+      return launch_eval_lds<KS, 8, 2>(ctx, coef, S, out, ring, flags, sums);
     case SF_EVAL_KERNEL_LDS16H:
-      return launch_eval_lds<KS, 16, 2>(ctx, coef, S, out, ring, flags);
+      return launch_eval_lds<KS, 16, 2>(ctx, coef, S, out, ring, flags, sums);
     case SF_EVAL_KERNEL_TILE3:
       // below 8 k-steps the register tile fits 4 waves/SIMD anyway
       return launch_eval_ks<KS, (KS >= 8 ? 3 : 2)>(ctx, coef, cxx, cyy, S, out,
-                                                   ring, flags);
+                                                   ring, flags, sums);
     default:
-      return launch_eval_ks<KS, 2>(ctx, coef, cxx, cyy, S, out, ring, flags);
+      return launch_eval_ks<KS, 2>(ctx, coef, cxx, cyy, S, out, ring, flags, sums);
   }
 }
 
 int launch_eval(sf_ctx* ctx, const double* coef, const double* cxx,
                 const double* cyy, int64_t S, float* out, int64_t ring,
-                unsigned flags) {
+                unsigned flags, unsigned long long* sums) {
   // zero k-step padding (SF_OPT_EVAL_KS_PAD) only for the LDS-staged
   // kernels, which take the real k-step count for their Cpix indexing
   const int v = pick_eval_kernel(ctx, cxx != nullptr, flags,
@@ -587,7 +622,7 @@ int launch_eval(sf_ctx* ctx, const double* coef, const double* cxx,
   switch (ks) {
 #define SF_KS(k) \
   case k:        \
-    return launch_eval_pick<k>(ctx, coef, cxx, cyy, S, out, ring, flags);
+    return launch_eval_pick<k>(ctx, coef, cxx, cyy, S, out, ring, flags, sums);
     SF_KS(1) SF_KS(2) SF_KS(3) SF_KS(4) SF_KS(5) SF_KS(6) SF_KS(7) SF_KS(8)
     SF_KS(9) SF_KS(10) SF_KS(11) SF_KS(12) SF_KS(13) SF_KS(14) SF_KS(15)
 #undef SF_KS

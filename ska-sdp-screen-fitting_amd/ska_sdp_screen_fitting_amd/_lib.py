@@ -50,7 +50,8 @@ EXPORTED = (
     "sf_synchronize", "sf_set_option", "sf_get_eval_kernel", "sf_alloc", "sf_free", "sf_copy_h2d", "sf_copy_d2h",
     "sf_set_basis", "sf_get_basis", "sf_kl_fit", "sf_get_fit_stats",
     "sf_stream_create", "sf_stream_destroy", "sf_device_cus",
-    "sf_set_grid", "sf_kl_eval", "sf_kl_eval_gain", "sf_tess_fill",
+    "sf_set_grid", "sf_kl_eval", "sf_kl_eval_gain", "sf_kl_eval_sums",
+    "sf_tess_fill",
 )
 
 
@@ -111,6 +112,8 @@ def load_library(path=None):
             "sf_device_cus": ([vp, ctypes.POINTER(c_int)], c_int),
             "sf_kl_eval_gain": ([vp, vp, vp, vp, i64, vp, i64, ctypes.c_uint],
                                 c_int),
+            "sf_kl_eval_sums": ([vp, vp, vp, vp, i64, vp, i64, ctypes.c_uint, vp],
+                                c_int),
             "sf_tess_fill": ([vp, vp, c_int, c_int, vp, vp, vp, c_int, i64, vp,
                               i64, c_dbl, ctypes.c_uint], c_int),
         }
@@ -130,7 +133,7 @@ def _check(rc, what):
 
 
 _TORCH_DTYPES = {np.float64: "torch.float64", np.float32: "torch.float32",
-                 np.int32: "torch.int32"}
+                 np.int32: "torch.int32", np.int64: "torch.int64"}
 
 
 def _dev(x, dtype, numel, name):
@@ -287,6 +290,22 @@ class Context:
             _dev(coef_yy, np.float64, n, "coef_yy"), int(S),
             _dev(out, np.float32, self._out_numel(S, ring), "out"), ring,
             int(flags)), "sf_kl_eval_gain")
+
+    def eval_sums(self, coef, S, out, sums, ring_slots=None, coef_xx=None,
+                  coef_yy=None,
+                  flags=SF_EVAL_NAN_SCRUB | SF_EVAL_FAST_SINCOS | SF_EVAL_NT_STORES):
+        """sf_kl_eval_sums: evaluate (phase, or gain with coef_xx / coef_yy)
+        and add each slot's output checksum (sum mod 2^64 of its 32-bit words)
+        to ``sums`` (int64 device tensor of >= S elements, zeroed by the
+        caller; int64 holds the uint64 bits)."""
+        ring = max(int(S if ring_slots is None else ring_slots), 1)
+        n = int(S) * self.D
+        _check(self.lib.sf_kl_eval_sums(
+            self.h, _dev(coef, np.float64, n, "coef"),
+            _dev(coef_xx, np.float64, n, "coef_xx"),
+            _dev(coef_yy, np.float64, n, "coef_yy"), int(S),
+            _dev(out, np.float32, self._out_numel(S, ring), "out"), ring,
+            int(flags), _dev(sums, np.int64, int(S), "sums")), "sf_kl_eval_sums")
 
     def tess_fill(self, labels, nx, ny, phase, D, S, out, ring_slots=None,
                   amp_xx=None, amp_yy=None, smooth_pix=0.0,
