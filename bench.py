@@ -207,7 +207,7 @@ def sampled_slots_check(ctx, torch, dev, setup, coef, N, flags, slot_sums,
             err = max(err, float((got - want)[:, live].abs().max()))
         if slot_sums is not None:
             h = int((one.view(torch.int32).to(torch.int64) & 0xFFFFFFFF).sum())
-            sums_ok &= (h * n_evals) % 2 ** 64 == int(slot_sums[k]) % 2 ** 64
+            sums_ok &= (h * n_evals) % 2 ** 32 == int(slot_sums[k]) % 2 ** 32
     tol = 2e-6 if fast else 1e-6
     res = {"slots": slots, "max_abs_err_vs_fp64": err, "tol": tol,
            "ok": err <= tol}
@@ -324,7 +324,7 @@ def main():
     # through the HBM ring and every slot's checksum is accumulated
     checksum = args.checksum == "on" or (args.checksum == "auto"
                                          and args.workload in ("config4", "config5"))
-    slot_sums = torch.zeros(S, dtype=torch.int64, device=dev) if checksum else None
+    slot_sums = torch.zeros(S, dtype=torch.int32, device=dev) if checksum else None
 
     def fit(c, fs):
         t0, t1 = bounds[c]

@@ -210,16 +210,17 @@ int sf_kl_eval_gain(sf_ctx* ctx, const double* coef_phase,
                     const double* coef_xx, const double* coef_yy, int64_t S,
                     float* out, int64_t ring_slots, unsigned flags);
 /* sf_kl_eval / sf_kl_eval_gain (coef_xx = coef_yy = NULL: phase screens)
- * that also ADD to slot_sums[s] (device, uint64, zeroed by the caller) the
- * checksum of slot s's output: the sum mod 2^64 of the 4 N^2 32-bit words
- * written for it (as stored, after the NaN scrub / byte swap).  Order-free
+ * that also ADD, mod 2^32, to slot_sums[s] (device, uint32, zeroed by the
+ * caller) the checksum of slot s's output: the sum mod 2^32 of the 4 N^2
+ * 32-bit words written for it (as stored, after the NaN scrub / byte swap;
+ * SURVEY.md §8(d) "per-slot sum of fp32 words").  Order-free
  * integer sums, so a slot streamed through a ring in a large run and the same
  * slot evaluated alone give the same value: the discard + checksum mode of
  * volumes that do not fit HBM. */
 int sf_kl_eval_sums(sf_ctx* ctx, const double* coef_phase,
                     const double* coef_xx, const double* coef_yy, int64_t S,
                     float* out, int64_t ring, unsigned flags,
-                    uint64_t* slot_sums);
+                    uint32_t* slot_sums);
 
 /*
  * Tessellated (Voronoi) screens: fill every pixel with the values of the

@@ -414,7 +414,7 @@ int sf_kl_eval_gain(sf_ctx* ctx, const double* coef_phase,
 int sf_kl_eval_sums(sf_ctx* ctx, const double* coef_phase,
                     const double* coef_xx, const double* coef_yy, int64_t S,
                     float* out, int64_t ring, unsigned flags,
-                    uint64_t* slot_sums) {
+                    uint32_t* slot_sums) {
   SF_REQUIRE(ctx && ctx->n_pix > 0 && ctx->d_cfrag, SF_EINVAL,
              "sf_kl_eval_sums: call sf_set_grid first");
   SF_REQUIRE(coef_phase && out && slot_sums && S >= 0 && ring >= 1,
@@ -424,7 +424,7 @@ int sf_kl_eval_sums(sf_ctx* ctx, const double* coef_phase,
   if (S == 0) return SF_OK;
   SF_HIP(hipSetDevice(ctx->device));
   return sf::launch_eval(ctx, coef_phase, coef_xx, coef_yy, S, out, ring, flags,
-                         reinterpret_cast<unsigned long long*>(slot_sums));
+                         reinterpret_cast<unsigned*>(slot_sums));
 }
 
 int sf_tess_fill(sf_ctx* ctx, const int32_t* labels, int nx, int ny,

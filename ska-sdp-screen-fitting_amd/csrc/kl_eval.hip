@@ -148,12 +148,21 @@ __device__ __forceinline__ float bswapf(float x) {
   return __uint_as_float(__builtin_bswap32(__float_as_uint(x)));
 }
 
-// Per-slot output checksum (sf_kl_eval_sums): the sum, mod 2^64, of the
+// Per-slot output checksum (sf_kl_eval_sums): the sum, mod 2^32, of the
 // 32-bit words the slot's cube holds (as stored: after the NaN scrub and any
 // byte swap).  Integer adds commute, so the value does not depend on which
-// lanes / waves / workgroups contribute in which order.
-__device__ __forceinline__ unsigned long long fbits(float x) {
-  return (unsigned long long)__float_as_uint(x);
+// lanes / waves / workgroups contribute in which order.  32-bit wrap-around
+// adds (v_add3_u32 chains) keep the epilogue cost at ~0.5 VALU op per word.
+__device__ __forceinline__ unsigned fbits(float x) { return __float_as_uint(x); }
+
+// Sum over the 16 lanes of each DPP row (every lane of the row receives it):
+// VALU-only butterflies, no LDS round trips.
+__device__ __forceinline__ unsigned row_sum16(unsigned v) {
+  v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad [1,0,3,2]
+  v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad [2,3,0,1]
+  v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false);  // row_ror:4
+  v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+  return v;
 }
 
 template <bool NT>
@@ -175,7 +184,7 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
     const double* __restrict__ coef_xx, const double* __restrict__ coef_yy,
     int D, int64_t S, int64_t P, int64_t n_pb, int64_t n_sc, int chunk_groups,
     float* __restrict__ out, int64_t ring, unsigned flags,
-    unsigned long long* __restrict__ sums) {
+    unsigned* __restrict__ sums) {
   const int l = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   // XCD-aware block -> (pixel block, slot chunk)
@@ -270,7 +279,7 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
           }
         }
         float* o = out + ((s % ring) * 4) * P + p0;
-        unsigned long long cs = 0ull;
+        unsigned cs = 0u;
         if (VEC4) {
           // P % 4 == 0: a lane's 4 pixels are all inside the grid or all out
           // (the last wave block of a grid that is not a multiple of 64)
@@ -279,7 +288,14 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
             for (int q = 0; q < 4; ++q) {
               const v4f v = {pv[q][0], pv[q][1], pv[q][2], pv[q][3]};
               store4<NT>(o + q * P, v);
-              if (sums) cs += (fbits(v[0]) + fbits(v[1])) + (fbits(v[2]) + fbits(v[3]));
+            }
+            if (sums) {
+              // phase screens store (cos, sin) twice: sum the planes once
+#pragma unroll
+              for (int q = 0; q < (GAIN ? 4 : 2); ++q)
+#pragma unroll
+                for (int t = 0; t < kTiles; ++t) cs += fbits(pv[q][t]);
+              if (!GAIN) cs *= 2u;
             }
           }
         } else {
@@ -295,9 +311,8 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
           }
         }
         if (sums) {
-          // the 16 lanes of this slot row hold its 64 pixels of the wave
-#pragma unroll
-          for (int m = 1; m < 16; m <<= 1) cs += __shfl_xor(cs, m, 64);
+          // the 16 lanes of this slot row (one DPP row) hold its 64 pixels
+          cs = row_sum16(cs);
           if ((l & 15) == 0) atomicAdd(sums + s, cs);
         }
       }
@@ -333,7 +348,7 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
     const double* __restrict__ cfrag, const double* __restrict__ coef, int D,
     int ks_real, int64_t S, int64_t P, int64_t n_pb, int64_t n_sc,
     int chunk_groups, float* __restrict__ out, int64_t ring, unsigned flags,
-    int sleep, unsigned long long* __restrict__ sums) {
+    int sleep, unsigned* __restrict__ sums) {
   using L = EvalLds<NW, TPW>;
   __shared__ float tile[2][16][L::kStride];
   const int l = threadIdx.x & 63;
@@ -441,15 +456,19 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
         }
         if (sums) {
           // planes 0 / 2 hold cos, 1 / 3 sin: every value is stored twice
-          unsigned long long cs = 0ull;
+          unsigned cs = 0u;
 #pragma unroll
           for (int c = 0; c < L::kChunks; ++c)
             if (pix0 + c * 256 + 4 * l < P)
 #pragma unroll
-              for (int e = 0; e < 4; ++e) cs += 2ull * (fbits(cv[c][e]) + fbits(sv[c][e]));
-#pragma unroll
-          for (int m = 1; m < 64; m <<= 1) cs += __shfl_xor(cs, m, 64);
-          if (l == 0) atomicAdd(sums + s, cs);
+              for (int e = 0; e < 4; ++e) cs += fbits(cv[c][e]) + fbits(sv[c][e]);
+          cs = row_sum16(2u * cs);
+          // the 4 row totals, uniform (scalar) values
+          const unsigned tot = (unsigned)__builtin_amdgcn_readlane((int)cs, 0) +
+                               (unsigned)__builtin_amdgcn_readlane((int)cs, 16) +
+                               (unsigned)__builtin_amdgcn_readlane((int)cs, 32) +
+                               (unsigned)__builtin_amdgcn_readlane((int)cs, 48);
+          if (l == 0) atomicAdd(sums + s, tot);
         }
       }
     }
@@ -487,7 +506,7 @@ template <int KS, int MINW>
 static int launch_eval_ks(sf_ctx* ctx, const double* coef,
                           const double* cxx, const double* cyy, int64_t S,
                           float* out, int64_t ring, unsigned flags,
-                          unsigned long long* sums) {
+                          unsigned* sums) {
   const int64_t P = ctx->n_pix;
   const int64_t n_pb = ctx->n_pix_blocks;
   // slot chunk per workgroup: 16 groups of 16 slots (1 MiB of output at
@@ -530,7 +549,7 @@ static int launch_eval_ks(sf_ctx* ctx, const double* coef,
 template <int KS, int NW, int TPW>
 static int launch_eval_lds(sf_ctx* ctx, const double* coef, int64_t S,
                            float* out, int64_t ring, unsigned flags,
-                           unsigned long long* sums) {
+                           unsigned* sums) {
   const int64_t P = ctx->n_pix;
   const int64_t run = EvalLds<NW, TPW>::kRun;
   const int64_t n_pb = (P + run - 1) / run;
@@ -584,7 +603,7 @@ template <int KS>
 static int launch_eval_pick(sf_ctx* ctx, const double* coef, const double* cxx,
                             const double* cyy, int64_t S, float* out,
                             int64_t ring, unsigned flags,
-                            unsigned long long* sums) {
+                            unsigned* sums) {
   const int v = pick_eval_kernel(ctx, cxx != nullptr, flags,
                                  (reinterpret_cast<uintptr_t>(out) & 15) == 0);
   switch (v) {
@@ -609,7 +628,7 @@ static int launch_eval_pick(sf_ctx* ctx, const double* coef, const double* cxx,
 
 int launch_eval(sf_ctx* ctx, const double* coef, const double* cxx,
                 const double* cyy, int64_t S, float* out, int64_t ring,
-                unsigned flags, unsigned long long* sums) {
+                unsigned flags, unsigned* sums) {
   // zero k-step padding (SF_OPT_EVAL_KS_PAD) only for the LDS-staged
   // kernels, which take the real k-step count for their Cpix indexing
   const int v = pick_eval_kernel(ctx, cxx != nullptr, flags,

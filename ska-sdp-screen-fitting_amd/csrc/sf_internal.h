@@ -115,7 +115,7 @@ int pick_eval_kernel(const sf_ctx* ctx, bool gain, unsigned flags,
                      bool out_aligned16);
 int launch_eval(sf_ctx* ctx, const double* coef, const double* cxx,
                 const double* cyy, int64_t S, float* out, int64_t ring,
-                unsigned flags, unsigned long long* sums);
+                unsigned flags, unsigned* sums);
 int launch_tess(sf_ctx* ctx, const int32_t* labels, int nx, int ny,
                 const double* phase, const double* amp_xx,
                 const double* amp_yy, int D, int64_t S, float* out,

@@ -295,9 +295,9 @@ class Context:
                   coef_yy=None,
                   flags=SF_EVAL_NAN_SCRUB | SF_EVAL_FAST_SINCOS | SF_EVAL_NT_STORES):
         """sf_kl_eval_sums: evaluate (phase, or gain with coef_xx / coef_yy)
-        and add each slot's output checksum (sum mod 2^64 of its 32-bit words)
-        to ``sums`` (int64 device tensor of >= S elements, zeroed by the
-        caller; int64 holds the uint64 bits)."""
+        and add (mod 2^32) each slot's output checksum -- the sum mod 2^32 of
+        its stored 32-bit words -- to ``sums`` (int32 device tensor of >= S
+        elements, zeroed by the caller; int32 holds the uint32 bits)."""
         ring = max(int(S if ring_slots is None else ring_slots), 1)
         n = int(S) * self.D
         _check(self.lib.sf_kl_eval_sums(
@@ -305,7 +305,7 @@ class Context:
             _dev(coef_xx, np.float64, n, "coef_xx"),
             _dev(coef_yy, np.float64, n, "coef_yy"), int(S),
             _dev(out, np.float32, self._out_numel(S, ring), "out"), ring,
-            int(flags), _dev(sums, np.int64, int(S), "sums")), "sf_kl_eval_sums")
+            int(flags), _dev(sums, np.int32, int(S), "sums")), "sf_kl_eval_sums")
 
     def tess_fill(self, labels, nx, ny, phase, D, S, out, ring_slots=None,
                   amp_xx=None, amp_yy=None, smooth_pix=0.0,

@@ -2,7 +2,7 @@
 of the evaluation (whose cubes cannot all
 stay resident).  Needs an MI355X: every test is marked ``gpu``.
 
-The checksum of a slot is the sum, mod 2^64, of the 32-bit words of its
+The checksum of a slot is the sum, mod 2^32, of the 32-bit words of its
 [4][ny][nx] cube as stored.  Checked against the same sum taken on the host
 from the cube the same launch wrote, for every kernel family, ragged grids,
 a ring smaller than the slot count, and the gain (amplitude) path; the cube
@@ -36,9 +36,10 @@ def ctx(dev):
 
 
 def host_sums(cube):
-    """[n, 4, ny, nx] float32 -> per-slot sum mod 2^64 of the 32-bit words."""
+    """[n, 4, ny, nx] float32 -> per-slot sum mod 2^32 of the 32-bit words."""
     w = np.ascontiguousarray(cube).view(np.uint32).reshape(cube.shape[0], -1)
-    return w.astype(np.uint64).sum(axis=1, dtype=np.uint64)
+    return (w.astype(np.uint64).sum(axis=1, dtype=np.uint64)
+            & np.uint64(0xFFFFFFFF)).astype(np.uint32)
 
 
 def grid_for(n_dir, grid, seed):
@@ -78,11 +79,11 @@ def test_eval_slot_sums(ctx, dev, n_dir, grid, kernel):
         ctx.set_option(SF_OPT_EVAL_KERNEL,
                        SF_EVAL_KERNEL_TILE if kernel == "tile" else SF_EVAL_KERNEL_AUTO)
         out = torch.full(shape, -7.0, dtype=torch.float32, device=dev)
-        sums = torch.zeros(S, dtype=torch.int64, device=dev)
+        sums = torch.zeros(S, dtype=torch.int32, device=dev)
         ctx.eval_sums(coef, S, out, sums, S, coef_xx=cxx, coef_yy=cyy, flags=flags)
         # a ring of 7 entries: the sums still cover every slot
         ring = torch.empty((7,) + shape[1:], dtype=torch.float32, device=dev)
-        sums7 = torch.zeros(S, dtype=torch.int64, device=dev)
+        sums7 = torch.zeros(S, dtype=torch.int32, device=dev)
         ctx.eval_sums(coef, S, ring, sums7, 7, coef_xx=cxx, coef_yy=cyy, flags=flags)
         plain = torch.full(shape, -7.0, dtype=torch.float32, device=dev)
         if gain:
@@ -93,9 +94,9 @@ def test_eval_slot_sums(ctx, dev, n_dir, grid, kernel):
     finally:
         ctx.set_option(SF_OPT_EVAL_KERNEL, SF_EVAL_KERNEL_AUTO)
     o = out.cpu().numpy()
-    got = sums.cpu().numpy().view(np.uint64)
+    got = sums.cpu().numpy().view(np.uint32)
     np.testing.assert_array_equal(got, host_sums(o))
-    np.testing.assert_array_equal(sums7.cpu().numpy().view(np.uint64), got)
+    np.testing.assert_array_equal(sums7.cpu().numpy().view(np.uint32), got)
     np.testing.assert_array_equal(o.view(np.uint32), plain.cpu().numpy().view(np.uint32))
 
 
@@ -107,9 +108,9 @@ def test_eval_sums_rejects_bad_operands(ctx, dev):
     coef = torch.zeros((S, 6), dtype=torch.float64, device=dev)
     out = torch.empty((S, 4, 16, 16), dtype=torch.float32, device=dev)
     with pytest.raises(TypeError):
-        ctx.eval_sums(coef, S, out, torch.zeros(S, dtype=torch.int32, device=dev))
+        ctx.eval_sums(coef, S, out, torch.zeros(S, dtype=torch.int64, device=dev))
     with pytest.raises(ValueError):
-        ctx.eval_sums(coef, S, out, torch.zeros(S - 1, dtype=torch.int64, device=dev))
+        ctx.eval_sums(coef, S, out, torch.zeros(S - 1, dtype=torch.int32, device=dev))
 
 
 def test_config5_shape_streamed_slots_vs_oracle(ctx, dev):
@@ -128,10 +129,10 @@ def test_config5_shape_streamed_slots_vs_oracle(ctx, dev):
     coef = torch.from_numpy(coef_np).to(dev)
     flags = SF_EVAL_NAN_SCRUB | SF_EVAL_FAST_SINCOS | SF_EVAL_NT_STORES
     ring = torch.empty((4, 4, N, N), dtype=torch.float32, device=dev)
-    sums = torch.zeros(S, dtype=torch.int64, device=dev)
+    sums = torch.zeros(S, dtype=torch.int32, device=dev)
     ctx.eval_sums(coef, S, ring, sums, 4, flags=flags)
     torch.cuda.synchronize()
-    got = sums.cpu().numpy().view(np.uint64)
+    got = sums.cpu().numpy().view(np.uint32)
     cpix = okl.cpix_matrix(pp, x, y)
     for k in (0, 29, 63):
         one = torch.empty((1, 4, N, N), dtype=torch.float32, device=dev)
