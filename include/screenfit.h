@@ -136,6 +136,7 @@ int sf_device_cus(sf_ctx* ctx, int* n_cu);
 #define SF_EVAL_KERNEL_LDS8H 5 /* LDS-staged, 2 MFMA tiles per wave (large D) */
 #define SF_EVAL_KERNEL_LDS16H 6
 #define SF_EVAL_KERNEL_TILE3 7 /* register tile at 3 waves per SIMD */
+#define SF_EVAL_KERNEL_SHB 8 /* register tile, Cpix shared in LDS by 4 waves */
 /* The evaluation kernel sf_kl_eval (gain = 0) or sf_kl_eval_gain (gain = 1)
  * runs for the current grid and these flags on a 16-byte aligned output
  * (one of SF_EVAL_KERNEL_TILE / _LDS4 / _LDS8 / _LDS16). */

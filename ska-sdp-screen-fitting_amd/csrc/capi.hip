@@ -156,7 +156,7 @@ int sf_set_option(sf_ctx* ctx, int option, int value) {
       ctx->force_general = value != 0;
       return SF_OK;
     case SF_OPT_EVAL_KERNEL:
-      SF_REQUIRE(value >= SF_EVAL_KERNEL_AUTO && value <= SF_EVAL_KERNEL_TILE3,
+      SF_REQUIRE(value >= SF_EVAL_KERNEL_AUTO && value <= SF_EVAL_KERNEL_SHB,
                  SF_EINVAL, "sf_set_option: unknown evaluation kernel");
       ctx->eval_kernel = value;
       return SF_OK;

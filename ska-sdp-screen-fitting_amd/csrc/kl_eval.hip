@@ -178,38 +178,62 @@ __device__ __forceinline__ double amp10(double x) {
   return exp10(x);
 }
 
-template <int KS, int MINW, bool VEC4, bool FAST, bool NT, bool GAIN>
+// SHB ("shared B"): the 4 waves of a workgroup share ONE 64-pixel block,
+// whose Cpix fragments sit in LDS (KS x 2 KiB) instead of 8*KS registers per
+// wave, and take its 16-slot groups round-robin -- the register tile at
+// ~half the VGPRs, so large D (config 5: D = 50) runs 4 waves per SIMD
+// without spilling; same MFMA operands in the same order, same bits.
+template <int KS, int MINW, bool VEC4, bool FAST, bool NT, bool GAIN,
+          bool SHB = false>
 __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
     const double* __restrict__ cfrag, const double* __restrict__ coef,
     const double* __restrict__ coef_xx, const double* __restrict__ coef_yy,
     int D, int64_t S, int64_t P, int64_t n_pb, int64_t n_sc, int chunk_groups,
     float* __restrict__ out, int64_t ring, unsigned flags,
     unsigned* __restrict__ sums) {
+  constexpr int kFrag = KS * kTiles * 64;  // Cpix doubles of a wave pixel block
+  __shared__ double bsh[SHB ? kFrag : 1];
   const int l = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
-  // XCD-aware block -> (pixel block, slot chunk)
+  // XCD-aware block -> (pixel block, slot chunk); SHB: n_pb counts 64-pixel
+  // wave blocks, else 256-pixel workgroup blocks
   const int64_t n_blocks = n_pb * n_sc;
   for (int64_t bb = blockIdx.x; bb < n_blocks; bb += gridDim.x) {
     int64_t pb, sc;
     eval_block(bb, n_pb, pb, sc, flags);
-    if (sc >= n_sc) continue;
-    const int64_t wpb = pb * kEvalWaves + w;
+    if (sc >= n_sc) continue;  // uniform per workgroup
+    const int64_t wpb = SHB ? pb : pb * kEvalWaves + w;
     const int64_t p0 = wpb * kWavePix + (int64_t)(l & 15) * kTiles;
+    if constexpr (SHB) {
+      __syncthreads();  // the previous item's reads of bsh are done
+      if (wpb * kWavePix < P)
+        for (int i = threadIdx.x; i < kFrag; i += 256) bsh[i] = cfrag[wpb * kFrag + i];
+      __syncthreads();
+    }
     if (wpb * kWavePix >= P) continue;
 
-    double bf[KS][kTiles];
+    double bf[SHB ? 1 : KS][kTiles];
+    if constexpr (!SHB) {
 #pragma unroll
-    for (int kk = 0; kk < KS; ++kk)
+      for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
-      for (int t = 0; t < kTiles; ++t)
-        bf[kk][t] = cfrag[((wpb * KS + kk) * kTiles + t) * 64 + l];
+        for (int t = 0; t < kTiles; ++t)
+          bf[kk][t] = cfrag[((wpb * KS + kk) * kTiles + t) * 64 + l];
+    }
+    auto bval = [&](int kk, int t) -> double {
+      if constexpr (SHB) return bsh[(kk * kTiles + t) * 64 + l];
+      else return bf[kk][t];
+    };
 
     const bool scrub = flags & SF_EVAL_NAN_SCRUB;
     const bool be = flags & SF_EVAL_BIG_ENDIAN;
     const int64_t slot_base = sc * (int64_t)chunk_groups * 16;
-    for (int g = 0; g < chunk_groups; ++g) {
+    for (int g = SHB ? w : 0; g < chunk_groups; g += SHB ? kEvalWaves : 1) {
       const int64_t s0 = slot_base + (int64_t)g * 16;
       if (s0 >= S) break;
+      // SHB: keep the Cpix reads inside the loop (in LDS, not hoisted into
+      // registers, which is the point)
+      if constexpr (SHB) asm volatile("" ::: "memory");
       double af[KS];
       {
         const int64_t s = s0 + (l & 15);
@@ -226,7 +250,7 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
       for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
         for (int t = 0; t < kTiles; ++t)
-          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[kk], bf[kk][t],
+          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[kk], bval(kk, t),
                                                         acc[t], 0, 0, 0);
       // gain: the XX / YY log-amplitude screens share the pixel basis
       v4d accx[GAIN ? kTiles : 1], accy[GAIN ? kTiles : 1];
@@ -245,8 +269,8 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
           const double ay = ok ? coef_yy[s * D + d] : 0.0;
 #pragma unroll
           for (int t = 0; t < kTiles; ++t) {
-            accx[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ax, bf[kk][t], accx[t], 0, 0, 0);
-            accy[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ay, bf[kk][t], accy[t], 0, 0, 0);
+            accx[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ax, bval(kk, t), accx[t], 0, 0, 0);
+            accy[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ay, bval(kk, t), accy[t], 0, 0, 0);
           }
         }
       }
@@ -546,6 +570,36 @@ static int launch_eval_ks(sf_ctx* ctx, const double* coef,
   return SF_OK;
 }
 
+// SHB register tile (phase screens, float4-aligned output): one workgroup
+// per (64-pixel wave block, chunk of 4 x 16 groups of 16 slots)
+template <int KS>
+static int launch_eval_shb(sf_ctx* ctx, const double* coef, int64_t S,
+                           float* out, int64_t ring, unsigned flags,
+                           unsigned* sums) {
+  const int64_t P = ctx->n_pix;
+  const int64_t n_wpb = ctx->n_pix_blocks * kEvalWaves;
+  int groups = 64;
+  while (groups > 4 && n_wpb * ((S + 16 * groups - 1) / (16 * groups)) < 4096)
+    groups >>= 1;
+  const int64_t n_sc = (S + 16 * groups - 1) / (16 * groups);
+  const int64_t nblk = eval_grid(ctx, n_wpb, n_sc, 256);
+  const bool fast = flags & SF_EVAL_FAST_SINCOS;
+  const bool nt = flags & SF_EVAL_NT_STORES;
+#define SF_LAUNCH_SHB(F, N)                                                     \
+  hipLaunchKernelGGL((kl_eval_kernel<KS, 4, true, F, N, false, true>),          \
+                     dim3((unsigned)nblk), dim3(256), 0, ctx->stream,           \
+                     ctx->d_cfrag, coef, nullptr, nullptr, ctx->D, S, P, n_wpb, \
+                     n_sc, groups, out, ring, flags, sums)
+  if (fast) {
+    if (nt) SF_LAUNCH_SHB(true, true); else SF_LAUNCH_SHB(true, false);
+  } else {
+    if (nt) SF_LAUNCH_SHB(false, true); else SF_LAUNCH_SHB(false, false);
+  }
+#undef SF_LAUNCH_SHB
+  SF_HIP(hipGetLastError());
+  return SF_OK;
+}
+
 template <int KS, int NW, int TPW>
 static int launch_eval_lds(sf_ctx* ctx, const double* coef, int64_t S,
                            float* out, int64_t ring, unsigned flags,
@@ -586,17 +640,22 @@ int pick_eval_kernel(const sf_ctx* ctx, bool gain, unsigned flags,
   const bool lds_ok = !gain && (flags & SF_EVAL_FAST_SINCOS) &&
                       (ctx->n_pix % 4 == 0) && out_aligned16;
   const int opt = ctx->eval_kernel;
+  if (opt == SF_EVAL_KERNEL_SHB)
+    return (!gain && ctx->n_pix % 4 == 0 && out_aligned16) ? opt : SF_EVAL_KERNEL_TILE;
   if (opt == SF_EVAL_KERNEL_TILE || opt == SF_EVAL_KERNEL_TILE3) return opt;
   if (!lds_ok) return SF_EVAL_KERNEL_TILE;
   if (opt != SF_EVAL_KERNEL_AUTO) return opt;
   // measured on MI355X (tools/eval_variants.py, profiles/round1d_eval_variants.txt):
   // long store runs win while the contraction is light; from ksteps 8 on
   // (D > 28) the per-group barrier serialises MFMA and stores and the
-  // register-tile kernel is faster, at 3 waves per SIMD from ksteps 10 on
-  // (D > 36: the Cpix fragments alone take 8*ksteps VGPRs)
+  // register-tile kernel is faster; from ksteps 10 on (D > 36: the Cpix
+  // fragments alone take 8*ksteps VGPRs) the tile with its Cpix shared in LDS
+  // (96 VGPRs, 5 waves/SIMD at D = 50) beats the register-resident one at 3
+  // waves/SIMD (168 VGPRs + spills): +5 % at D = 50, 512^2
+  // (profiles/round1h_eval_shb.txt)
   if (ctx->ksteps <= 2) return SF_EVAL_KERNEL_LDS4;
   if (ctx->ksteps <= 7) return SF_EVAL_KERNEL_LDS16;
-  return ctx->ksteps <= 9 ? SF_EVAL_KERNEL_TILE : SF_EVAL_KERNEL_TILE3;
+  return ctx->ksteps <= 9 ? SF_EVAL_KERNEL_TILE : SF_EVAL_KERNEL_SHB;
 }
 
 template <int KS>
@@ -617,6 +676,8 @@ static int launch_eval_pick(sf_ctx* ctx, const double* coef, const double* cxx,
       return launch_eval_lds<KS, 8, 2>(ctx, coef, S, out, ring, flags, sums);
     case SF_EVAL_KERNEL_LDS16H:
       return launch_eval_lds<KS, 16, 2>(ctx, coef, S, out, ring, flags, sums);
+    case SF_EVAL_KERNEL_SHB:
+      return launch_eval_shb<KS>(ctx, coef, S, out, ring, flags, sums);
     case SF_EVAL_KERNEL_TILE3:
       // below 8 k-steps the register tile fits 4 waves/SIMD anyway
       return launch_eval_ks<KS, (KS >= 8 ? 3 : 2)>(ctx, coef, cxx, cyy, S, out,
@@ -633,7 +694,8 @@ int launch_eval(sf_ctx* ctx, const double* coef, const double* cxx,
   // kernels, which take the real k-step count for their Cpix indexing
   const int v = pick_eval_kernel(ctx, cxx != nullptr, flags,
                                  (reinterpret_cast<uintptr_t>(out) & 15) == 0);
-  const bool lds = v != SF_EVAL_KERNEL_TILE && v != SF_EVAL_KERNEL_TILE3;
+  const bool lds = v != SF_EVAL_KERNEL_TILE && v != SF_EVAL_KERNEL_TILE3 &&
+                   v != SF_EVAL_KERNEL_SHB;
   int ks = ctx->ksteps + (lds ? ctx->eval_ks_pad : 0);
   flags &= ~kEvalXcdInterleave;
   if (ctx->eval_xcd_map > 0) flags |= kEvalXcdInterleave;

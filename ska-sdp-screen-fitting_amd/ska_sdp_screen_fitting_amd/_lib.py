@@ -36,13 +36,15 @@ SF_EVAL_KERNEL_LDS16 = 4
 SF_EVAL_KERNEL_LDS8H = 5
 SF_EVAL_KERNEL_LDS16H = 6
 SF_EVAL_KERNEL_TILE3 = 7
+SF_EVAL_KERNEL_SHB = 8
 EVAL_KERNEL_NAMES = {SF_EVAL_KERNEL_TILE: "kl_eval_kernel",
                      SF_EVAL_KERNEL_LDS4: "kl_eval_lds_kernel<4 waves>",
                      SF_EVAL_KERNEL_LDS8: "kl_eval_lds_kernel<8 waves>",
                      SF_EVAL_KERNEL_LDS16: "kl_eval_lds_kernel<16 waves>",
                      SF_EVAL_KERNEL_LDS8H: "kl_eval_lds_kernel<8 waves, 2 tiles>",
                      SF_EVAL_KERNEL_LDS16H: "kl_eval_lds_kernel<16 waves, 2 tiles>",
-                     SF_EVAL_KERNEL_TILE3: "kl_eval_kernel<3 waves/SIMD>"}
+                     SF_EVAL_KERNEL_TILE3: "kl_eval_kernel<3 waves/SIMD>",
+                     SF_EVAL_KERNEL_SHB: "kl_eval_kernel<Cpix in LDS>"}
 
 # every symbol include/screenfit.h declares (checked by tests/test_capi.py)
 EXPORTED = (

@@ -19,7 +19,7 @@ from ska_sdp_screen_fitting_amd import get_context  # noqa: E402
 from ska_sdp_screen_fitting_amd._lib import (  # noqa: E402
     SF_EVAL_FAST_SINCOS, SF_EVAL_KERNEL_AUTO, SF_EVAL_KERNEL_LDS4,
     SF_EVAL_KERNEL_LDS8, SF_EVAL_KERNEL_LDS8H, SF_EVAL_KERNEL_LDS16,
-    SF_EVAL_KERNEL_LDS16H, SF_EVAL_KERNEL_TILE, SF_EVAL_KERNEL_TILE3,
+    SF_EVAL_KERNEL_LDS16H, SF_EVAL_KERNEL_SHB, SF_EVAL_KERNEL_TILE, SF_EVAL_KERNEL_TILE3,
     SF_EVAL_NAN_SCRUB, SF_EVAL_NT_STORES, SF_OPT_EVAL_KERNEL,
     SF_OPT_EVAL_KS_PAD, SF_OPT_EVAL_SLEEP, SF_OPT_EVAL_XCD_MAP)
 
@@ -27,7 +27,7 @@ KERNELS = {"auto": SF_EVAL_KERNEL_AUTO, "tile": SF_EVAL_KERNEL_TILE,
            "tile3": SF_EVAL_KERNEL_TILE3,
            "lds4": SF_EVAL_KERNEL_LDS4, "lds8": SF_EVAL_KERNEL_LDS8,
            "lds16": SF_EVAL_KERNEL_LDS16, "lds8h": SF_EVAL_KERNEL_LDS8H,
-           "lds16h": SF_EVAL_KERNEL_LDS16H}
+           "lds16h": SF_EVAL_KERNEL_LDS16H, "shb": SF_EVAL_KERNEL_SHB}
 
 ap = argparse.ArgumentParser()
 ap.add_argument("shapes", nargs="*", default=["20:256"])
