@@ -648,14 +648,15 @@ int pick_eval_kernel(const sf_ctx* ctx, bool gain, unsigned flags,
   // measured on MI355X (tools/eval_variants.py, profiles/round1d_eval_variants.txt):
   // long store runs win while the contraction is light; from ksteps 8 on
   // (D > 28) the per-group barrier serialises MFMA and stores and the
-  // register-tile kernel is faster; from ksteps 10 on (D > 36: the Cpix
-  // fragments alone take 8*ksteps VGPRs) the tile with its Cpix shared in LDS
-  // (96 VGPRs, 5 waves/SIMD at D = 50) beats the register-resident one at 3
-  // waves/SIMD (168 VGPRs + spills): +5 % at D = 50, 512^2
-  // (profiles/round1h_eval_shb.txt)
+  // register-tile kernel is faster, at 3 waves per SIMD from ksteps 10 on
+  // (D > 36: the Cpix fragments alone take 8*ksteps VGPRs); from ksteps 12
+  // on (D > 44) the tile with its Cpix shared in LDS (96 VGPRs, 5 waves/SIMD
+  // at D = 50) beats it: +3-5 % at D = 50, -2 % at D = 40 (512^2;
+  // profiles/round1h_eval_shb.txt)
   if (ctx->ksteps <= 2) return SF_EVAL_KERNEL_LDS4;
   if (ctx->ksteps <= 7) return SF_EVAL_KERNEL_LDS16;
-  return ctx->ksteps <= 9 ? SF_EVAL_KERNEL_TILE : SF_EVAL_KERNEL_SHB;
+  if (ctx->ksteps <= 9) return SF_EVAL_KERNEL_TILE;
+  return ctx->ksteps <= 11 ? SF_EVAL_KERNEL_TILE3 : SF_EVAL_KERNEL_SHB;
 }
 
 template <int KS>
