@@ -64,9 +64,12 @@ def parse():
                     help="time chunks per step: the fit of chunk c+1 runs on a "
                          "second stream while chunk c is evaluated (1 = fit "
                          "then eval, serialised)")
-    ap.add_argument("--reserve-cus", type=int, default=16,
+    ap.add_argument("--reserve-cus", type=int, default=-1,
                     help="compute units the eval stream leaves to the fit "
-                         "stream (pipelined mode)")
+                         "stream (pipelined mode); -1 (default): 16 when "
+                         "D <= 32 (the fit then runs on exactly those), else 0 "
+                         "(at D = 50 the eval is compute-bound and the fit "
+                         "too heavy for 16 CUs: config 5 +8 %)")
     ap.add_argument("--fit-on-reserved", type=int, default=-1,
                     help="1: confine the fit stream to the reserved CUs "
                          "(pipelined mode); -1 (default): when D <= 32, where "
@@ -302,12 +305,15 @@ def main():
     # it runs on an unrestricted stream even when later fits are confined
     first_fit_stream = fit_stream
     if n_chunks > 1:
-        if args.reserve_cus > 0:
+        reserve_cus = args.reserve_cus
+        if reserve_cus < 0:
+            reserve_cus = 16 if D <= 32 else 0
+        if reserve_cus > 0:
             n_cu = ctx.device_cus()
-            step = max(1, n_cu // args.reserve_cus)
+            step = max(1, n_cu // reserve_cus)
             # k*step + k%8: one per XCD whether CUs are numbered XCD-major
             # or interleaved across the 8 XCDs
-            reserved = [min(n_cu - 1, k * step + k % 8) for k in range(args.reserve_cus)]
+            reserved = [min(n_cu - 1, k * step + k % 8) for k in range(reserve_cus)]
             masked_handle = ctx.stream_create(reserved)
             stream = torch.cuda.ExternalStream(masked_handle, device=dev)
             on_reserved = args.fit_on_reserved
