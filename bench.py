@@ -4,10 +4,12 @@
 One step = one pass of the hot path over one batch of synthetic input, on
 every GPU: the batched KL fit of all of the rank's slots (``sf_kl_fit``)
 followed by the KL pixel evaluation of all of them (``sf_kl_eval``) into an
-HBM ring of output cubes.  Workload per GPU = BASELINE.json configs[2]
-(64 ant x 100 time x 16 freq x 20 dir, KL 256^2 screen); with --gpus N the
-antenna axis grows to 64 N and is sharded (weak scaling, configs[3] shape at
-N=4), with only one-shot setup collectives.
+HBM ring of output cubes.  Default workload = BASELINE.json configs[3], the
+config the north_star's targets are quoted on: 256 ant x 1000 time x 32 freq
+x 20 dir, KL 256^2 screen, the antenna axis split over the --gpus N ranks
+(strong scaling; 8.19 M slots per step in total, discard + checksum mode).
+``--workload config3`` is configs[2] per GPU (weak scaling), ``config5``
+configs[4]'s per-GPU shard.  Only one-shot setup collectives.
 
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
@@ -48,9 +50,9 @@ STRONG = {"config4"}  # first field = stations of the whole job
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="config3", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="config4", choices=sorted(WORKLOADS))
     ap.add_argument("--ring-gb", type=float, default=16.0,
                     help="HBM ring for the output cubes (GiB)")
     ap.add_argument("--precise-sincos", action="store_true",
@@ -59,7 +61,13 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fits", action="store_true",
                     help="skip the FITS-cube wall-clock leg (configs 1-2)")
-    ap.add_argument("--cpu-workers", type=int, default=16)
+    ap.add_argument("--cpu-workers", type=int, default=0,
+                    help="CPU baseline pool size; 0 (default): every CPU this "
+                         "process may run on, capped at the 16 host cores a "
+                         "one-GPU box grants per GPU")
+    ap.add_argument("--no-side-legs", action="store_true",
+                    help="skip the untimed side measurements (fp64-sincos "
+                         "eval, fit alone on the whole chip)")
     ap.add_argument("--chunks", type=int, default=2,
                     help="time chunks per step: the fit of chunk c+1 runs on a "
                          "second stream while chunk c is evaluated (1 = fit "
@@ -145,17 +153,39 @@ def cpu_baseline(sol, setup, n_workers, slots_fit=64, slots_eval=192):
     n_ev = sum(r[2] for r in res)
     t_ev = sum(r[3] for r in res)
     per_slot = t_fit / n_fit + t_ev / n_ev  # core-seconds per slot (fit + eval)
+    P = len(setup["x"]) * len(setup["y"])
+    # the reference itself, timed during the survey on an 8-vCPU Xeon
+    # (SURVEY.md §6): calculate_kl_screen 8.5 us / pixel / slot / core,
+    # _fit_screen 68-92 us / slot (unflagged)
+    ref_slot_s = 8.5e-6 * P + 80e-6
     return {
         "value": n_workers / per_slot,
         "unit": "screen-slots/s",
         "cores": n_workers,
         "kind": "port",
+        "host_cpus": os.cpu_count(),
+        "affinity_cpus": _affinity(),
         "sample": (f"oracle (numpy fp64 restatement) on {n_fit} fit slots and "
                    f"{n_ev} {len(setup['x'])}^2 eval slots of the same workload, "
                    f"{n_workers} single-threaded workers, {wall:.1f} s wall; "
                    f"fit {t_fit / n_fit * 1e3:.3f} ms/slot/core, eval "
                    f"{t_ev / n_ev * 1e3:.1f} ms/slot/core"),
+        "reference_calibration": {
+            "note": ("the reference's own per-slot costs measured in the survey "
+                     "(SURVEY.md §6, 8-vCPU Xeon): calculate_kl_screen 8.5 us "
+                     "/ pixel / slot / core, _fit_screen ~80 us / slot; its "
+                     "Python loop is ~10x slower than this vectorised port"),
+            "ref_s_per_slot_core": ref_slot_s,
+            "ref_slots_per_s_at_cores": n_workers / ref_slot_s,
+        },
     }
+
+
+def _affinity():
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count()
 
 
 def fits_wallclock():
@@ -217,6 +247,85 @@ def sampled_slots_check(ctx, torch, dev, setup, coef, N, flags, slot_sums,
     if slot_sums is not None:
         res["checksums_match"] = bool(sums_ok)
         res["ok"] = res["ok"] and bool(sums_ok)
+    return res
+
+
+FP64_MFMA_PEAK_TFS = 78.6  # MI355X fp64 matrix peak (AMD spec, dense)
+
+
+def _profile_entry(name, workload, kernel):
+    """Entry of a profiles/<name>.json table (written by the tools/ that turn
+    rocprofv3 PMC passes into per-launch figures) for this workload and
+    evaluation kernel, or None."""
+    path = os.path.join(REPO, "profiles", name)
+    try:
+        tab = json.load(open(path))
+    except (ValueError, OSError):
+        return None
+    for e in tab.get("entries", []):
+        if e.get("workload") == workload and e.get("eval_kernel") == kernel:
+            return e
+    return None
+
+
+def mfma_line(kernel, launch_slots, P, D, launch_s, workload):
+    """fp64 MFMA work of one evaluation launch: executed flops (the k-steps
+    padded to a multiple of 4 directions) and the algorithmic 2 D flops per
+    pixel per slot, over the launch time, against the fp64 matrix peak; the
+    MFMA-busy fraction from PMC counters when profiles/mfma.json holds this
+    workload."""
+    ks = (D + 3) // 4
+    executed = launch_slots * P * 2.0 * 4 * ks
+    algo = launch_slots * P * 2.0 * D
+    res = {"kernel": kernel, "unit": "TFLOP/s", "peak": FP64_MFMA_PEAK_TFS,
+           "executed": executed / launch_s / 1e12,
+           "algorithmic": algo / launch_s / 1e12,
+           "flops_per_launch": executed}
+    res["frac"] = res["executed"] / FP64_MFMA_PEAK_TFS
+    e = _profile_entry("mfma.json", workload, kernel)
+    if e is not None:
+        res["busy_frac_pmc"] = e.get("mfma_busy_frac")
+        res["valu_busy_frac_pmc"] = e.get("valu_busy_frac")
+    return res
+
+
+def side_legs(ctx, torch, dev, stream, fit_stream, fit, coef, bounds, F, A,
+              D, P, out, ring, flags):
+    """Untimed side measurements after the timed steps: (1) the evaluation of
+    time chunk 0 with the fp64 sincos epilogue (--precise-sincos) beside the
+    default fp32 one, (2) the fit of chunk 0 alone on the whole chip.  HIP
+    events on the stream each runs on."""
+    from ska_sdp_screen_fitting_amd._lib import SF_EVAL_FAST_SINCOS
+    t0, t1 = bounds[0]
+    n = (t1 - t0) * F * A
+    c0 = coef[t0:t1].reshape(-1, D)
+    res = {}
+
+    def timed(fn, st, reps=2):
+        fn()  # warm (kernel choice, code object)
+        ms = []
+        for _ in range(reps):
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            fn()
+            e1.record(st)
+            torch.cuda.synchronize(dev)
+            ms.append(e0.elapsed_time(e1))
+        return float(np.mean(ms))
+
+    for name, fl in (("eval_fp32_sincos", flags),
+                     ("eval_fp64_sincos", flags & ~SF_EVAL_FAST_SINCOS)):
+        ctx.set_stream(stream.cuda_stream)
+        ms = timed(lambda: ctx.eval(c0, n, out, ring, fl), stream)
+        gbs = n * (16 * P + 8 * D) / ms / 1e6
+        res[name] = {"kernel": ctx.eval_kernel(fl), "slots": n,
+                     "launch_ms": ms, "slots_per_s": n / ms * 1e3,
+                     "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS}
+    ms = timed(lambda: fit(0, fit_stream), fit_stream)
+    res["fit_alone_whole_chip"] = {"slots": n, "ms": ms,
+                                   "slots_per_s": n / ms * 1e3}
+    ctx.set_stream(stream.cuda_stream)
     return res
 
 
@@ -427,22 +536,20 @@ def main():
                                   flags, slot_sums, args.warmup + args.steps,
                                   not args.precise_sincos)
 
+    side = {}
+    if not args.no_side_legs and not args.eval_only:
+        side = side_legs(ctx, torch, dev, stream, first_fit_stream, fit, coef,
+                         bounds, F, A, D, P, out, ring, flags)
+
     if rank == 0:
         algo_bytes = S * (16 * P + 8 * D)  # SURVEY.md §8(d), per step
         launch_bytes = algo_bytes / n_chunks  # per eval launch (equal chunks)
         achieved = launch_bytes / t_eval_launch / 1e9
         traffic = None
-        tpath = os.path.join(REPO, "profiles", "traffic.json")
-        if os.path.exists(tpath):
-            try:
-                tj = json.load(open(tpath))
-                if (tj.get("workload") == args.workload
-                        and tj.get("flags") == flags
-                        and tj.get("chunks", 1) == n_chunks
-                        and tj.get("eval_kernel") == eval_kernel_name):
-                    traffic = tj.get("hbm_bytes_per_launch")
-            except (ValueError, OSError):
-                traffic = None
+        tj = _profile_entry("traffic.json", args.workload, eval_kernel_name)
+        if (tj is not None and tj.get("flags") == flags
+                and tj.get("chunks", 1) == n_chunks):
+            traffic = tj.get("hbm_bytes_per_launch")
         line = {
             "metric": METRIC,
             "value": T * F * A_total * args.steps / elapsed,
@@ -477,6 +584,8 @@ def main():
                 "bytes_per_launch": launch_bytes,
                 "launch_ms": t_eval_launch * 1e3,
             },
+            "mfma": mfma_line(eval_kernel_name, S / n_chunks, P, D,
+                              t_eval_launch, args.workload),
             "stages_ms": {"fit": t_fit * 1e3, "eval": t_eval * 1e3,
                           "overlap": "fit(c+1) || eval(c), %d time chunks" % n_chunks
                           if n_chunks > 1 else "none"},
@@ -484,11 +593,13 @@ def main():
             "check": {"max_abs_cos2_plus_sin2_minus_1": unit_err,
                       "sampled_slots": sampled},
         }
+        if side:
+            line["side_legs"] = side
         if not args.no_fits and world == 1:
             line["fits_wallclock"] = fits_wallclock()
         if not args.no_cpu_baseline and world == 1:
-            line["cpu_baseline"] = cpu_baseline(
-                sol, setup, max(1, min(args.cpu_workers, os.cpu_count() or 1)))
+            nw = args.cpu_workers or min(16, _affinity() or 1)
+            line["cpu_baseline"] = cpu_baseline(sol, setup, max(1, nw))
         print(json.dumps(line), flush=True)
     # release the CU-masked stream before the HIP runtime tears down
     torch.cuda.synchronize(dev)

@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <type_traits>
 
 #include "sf_internal.h"
 
@@ -77,26 +78,56 @@ __global__ __launch_bounds__(256) void kl_cpix_kernel(
   cfrag[e] = v;
 }
 
-// sin / cos of a phase already reduced to [-pi, pi] (in fp64, then rounded
-// to float): quadrant split with a two-part pi/2 and Cephes' single-precision
-// minimax polynomials on [-pi/4, pi/4] -- branch-free, ~20 VALU ops, error
-// <= 2e-7 beyond the float rounding of the argument.  NaN in, NaN out.
-__device__ __forceinline__ void sincos_reduced(float r, float& s, float& c) {
-  const float q = rintf(r * 0.63661977236758134f);
-  float y = fmaf(-q, 1.5707963705062866f, r);
-  y = fmaf(-q, -4.3711390001862412e-08f, y);
-  const float z = y * y;
-  float ps = fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f);
-  ps = fmaf(z, ps, -1.6666654611e-1f);
-  ps = fmaf(y * z, ps, y);
-  float pc = fmaf(z, 2.443315711809948e-5f, -1.388731625493765e-3f);
-  pc = fmaf(z, pc, 4.166664568298827e-2f);
-  pc = fmaf(z * z, pc, fmaf(-0.5f, z, 1.0f));
-  const int iq = (int)q;
-  const float a = (iq & 1) ? pc : ps;
-  const float b = (iq & 1) ? ps : pc;
-  s = (iq & 2) ? -a : a;
-  c = ((iq + 1) & 2) ? -b : b;
+// Fast epilogue (SF_EVAL_FAST_SINCOS): the contraction runs on coefficients
+// pre-scaled by 1 / 2 pi, so it yields the phase in REVOLUTIONS; the fp64
+// reduction rev - rint(rev) to [-1/2, 1/2] is exact, the result is rounded to
+// float (<= 1.5e-8 rev = 9.4e-8 rad) and fed to the hardware v_sin_f32 /
+// v_cos_f32, whose argument is in revolutions (max |err| 1.25e-7 over
+// [-1/2, 1/2] measured on MI355X, profiles/round2a_coexec_probe.txt): ~7 VALU
+// issues per value instead of the ~25 of a polynomial sincos.  On gfx950 the
+// fp64 MFMA holds the SIMD's VALU for its whole 64 cycles (same probe: MFMA
+// and VALU waves on one SIMD take the SUM of their times), so every VALU
+// cycle of the epilogue adds to the contraction's.
+constexpr double kInv2Pi = 0.15915494309189535;
+
+// fp32 revolutions in [-1/2, 1/2] of a phase given in revolutions; NaN / Inf
+// -> 0 when scrubbing, i.e. cos 1 and sin 0 (screen.py:368-378 NaN scrub)
+__device__ __forceinline__ float rev_reduce(double rev, bool scrub) {
+  const float f = (float)(rev - rint(rev));
+  return (scrub && __builtin_isnan(f)) ? 0.0f : f;
+}
+
+// v_sin_f32 / v_cos_f32 return NaN for a NaN argument (checked by the
+// unscrubbed cases of tests/test_gpu_parity.py::test_eval_kernels_agree)
+__device__ __forceinline__ void sincos_rev(float f, float& s, float& c) {
+  s = __builtin_amdgcn_sinf(f);
+  c = __builtin_amdgcn_cosf(f);
+}
+
+// MFMA A fragments of a 16-slot group: lane l holds coef[s0 + (l & 15)]
+// [4 kk + (l >> 4)] for every k-step (0 past S or D), times `scale`.  The
+// loads are unconditional (clamped addresses, then a select), so all KS of
+// them are in flight together: a guarded load compiles to a branch around
+// it and a wait after it, i.e. KS serial round trips to L2 per group.
+template <int KS>
+__device__ __forceinline__ void load_coef(double (&af)[KS],
+                                          const double* __restrict__ coef,
+                                          int64_t s0, int64_t S, int D, int l,
+                                          double scale) {
+  const int64_t s = s0 + (l & 15);
+  const bool srow = s < S;
+  const double* row = coef + (srow ? s : S - 1) * D;
+  double v[KS];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) {
+    const int d = 4 * kk + (l >> 4);
+    v[kk] = row[d < D ? d : D - 1];
+  }
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) {
+    const int d = 4 * kk + (l >> 4);
+    af[kk] = (srow && d < D) ? v[kk] * scale : 0.0;
+  }
 }
 
 // Workgroup index -> (pixel block, slot chunk).  XCD-aware when the pixel
@@ -125,14 +156,12 @@ __device__ __forceinline__ void eval_block(int64_t bb, int64_t n_pb,
   }
 }
 
+// FAST: ph in revolutions (see rev_reduce); else ph in radians, fp64 sincos
 template <bool FAST>
-__device__ __forceinline__ void jones_sincos(double ph, float& s, float& c) {
+__device__ __forceinline__ void jones_sincos(double ph, float& s, float& c,
+                                             bool scrub) {
   if (FAST) {
-    // exact-ish fp64 reduction to [-pi, pi], then fp32 sincos
-    const double k = rint(ph * 0.15915494309189535);
-    double r = fma(-k, 6.283185307179586, ph);
-    r = fma(-k, 2.4492935982947064e-16, r);
-    sincos_reduced((float)r, s, c);
+    sincos_rev(rev_reduce(ph, scrub), s, c);
   } else {
     double sd, cd;
     sincos(ph, &sd, &cd);
@@ -194,7 +223,8 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
   constexpr int kFrag = KS * kTiles * 64;  // Cpix doubles of a wave pixel block
   __shared__ double bsh[SHB ? kFrag : 1];
   const int l = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
+  // wave index, wave-uniform: keeps slot / ring arithmetic on the SALU
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // XCD-aware block -> (pixel block, slot chunk); SHB: n_pb counts 64-pixel
   // wave blocks, else 256-pixel workgroup blocks
   const int64_t n_blocks = n_pb * n_sc;
@@ -235,14 +265,11 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
       // registers, which is the point)
       if constexpr (SHB) asm volatile("" ::: "memory");
       double af[KS];
-      {
-        const int64_t s = s0 + (l & 15);
-#pragma unroll
-        for (int kk = 0; kk < KS; ++kk) {
-          const int d = 4 * kk + (l >> 4);
-          af[kk] = (s < S && d < D) ? coef[s * D + d] : 0.0;
-        }
-      }
+      load_coef<KS>(af, coef, s0, S, D, l, FAST ? kInv2Pi : 1.0);
+      // ring slot of the group's first slot (S, ring < 2^31: launch_eval);
+      // the 16 rows follow it with at most one wrap when the ring is >= 16
+      // slots -- scalar, no per-lane 64-bit modulo
+      const uint32_t ring0 = (uint32_t)s0 % (uint32_t)ring;
       v4d acc[kTiles];
 #pragma unroll
       for (int t = 0; t < kTiles; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
@@ -255,36 +282,44 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
       // gain: the XX / YY log-amplitude screens share the pixel basis
       v4d accx[GAIN ? kTiles : 1], accy[GAIN ? kTiles : 1];
       if (GAIN) {
-        const int64_t s = s0 + (l & 15);
+        double ax[KS], ay[KS];
+        load_coef<KS>(ax, coef_xx, s0, S, D, l, 1.0);
+        load_coef<KS>(ay, coef_yy, s0, S, D, l, 1.0);
 #pragma unroll
         for (int t = 0; t < kTiles; ++t) {
           accx[t] = v4d{0.0, 0.0, 0.0, 0.0};
           accy[t] = v4d{0.0, 0.0, 0.0, 0.0};
         }
 #pragma unroll
-        for (int kk = 0; kk < KS; ++kk) {
-          const int d = 4 * kk + (l >> 4);
-          const bool ok = s < S && d < D;
-          const double ax = ok ? coef_xx[s * D + d] : 0.0;
-          const double ay = ok ? coef_yy[s * D + d] : 0.0;
+        for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
           for (int t = 0; t < kTiles; ++t) {
-            accx[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ax, bval(kk, t), accx[t], 0, 0, 0);
-            accy[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ay, bval(kk, t), accy[t], 0, 0, 0);
+            accx[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ax[kk], bval(kk, t), accx[t], 0, 0, 0);
+            accy[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ay[kk], bval(kk, t), accy[t], 0, 0, 0);
           }
-        }
       }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t s = s0 + acc_row(l, r);
-        if (s >= S) continue;  // uniform over the 16 lanes of a slot row
+      // one MFMA accumulator row: 4 slot rows x this lane's 4 pixels; BE
+      // (FITS byte order) as a compile-time branch of the whole row
+      auto row_out = [&](int r, auto be_tag) {
+        constexpr bool kBE = decltype(be_tag)::value;
+        const int row = acc_row(l, r);
+        const int64_t s = s0 + row;
+        if (s >= S) return;  // uniform over the 16 lanes of a slot row
+        uint32_t so = ring0 + (uint32_t)row;
+        if (ring >= 16) {
+          if (so >= (uint32_t)ring) so -= (uint32_t)ring;
+        } else {
+          so %= (uint32_t)ring;
+        }
         // planes 0..3 = Re XX, Im XX, Re YY, Im YY
         float pv[4][kTiles];
 #pragma unroll
         for (int t = 0; t < kTiles; ++t) {
           float sf, cf;
-          jones_sincos<FAST>(acc[t][r], sf, cf);
           if (GAIN) {
+            // a NaN phase stays NaN through A * cos and is scrubbed below,
+            // as the reference scrubs the product (screen.py:368-378)
+            jones_sincos<FAST>(acc[t][r], sf, cf, false);
             // reference: A (fp64) * cos (fp64), one cast at the FITS store
             const double ax = amp10<FAST>(accx[t][r]);
             const double ay = amp10<FAST>(accy[t][r]);
@@ -293,16 +328,19 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
             pv[2][t] = (float)(ay * (double)cf);
             pv[3][t] = (float)(ay * (double)sf);
           } else {
+            // FAST: NaN scrubbed on the reduced argument (cos 1, sin 0)
+            jones_sincos<FAST>(acc[t][r], sf, cf, scrub);
             pv[0][t] = pv[2][t] = cf;
             pv[1][t] = pv[3][t] = sf;
           }
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            if (scrub && isnan(pv[q][t])) pv[q][t] = (q & 1) ? 0.0f : 1.0f;
-            if (be) pv[q][t] = bswapf(pv[q][t]);
+            if (scrub && (GAIN || !FAST) && isnan(pv[q][t]))
+              pv[q][t] = (q & 1) ? 0.0f : 1.0f;
+            if (kBE) pv[q][t] = bswapf(pv[q][t]);
           }
         }
-        float* o = out + ((s % ring) * 4) * P + p0;
+        float* o = out + ((int64_t)so * 4) * P + p0;
         unsigned cs = 0u;
         if (VEC4) {
           // P % 4 == 0: a lane's 4 pixels are all inside the grid or all out
@@ -339,6 +377,13 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
           cs = row_sum16(cs);
           if ((l & 15) == 0) atomicAdd(sums + s, cs);
         }
+      };
+      if (be) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) row_out(r, std::true_type{});
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) row_out(r, std::false_type{});
       }
     }
   }  // workgroup walk
@@ -347,9 +392,9 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
 // LDS-staged variant (phase screens, fp32 sincos epilogue): the same MFMA
 // contraction, but the stores are re-mapped so that one wave writes long
 // contiguous runs.  A workgroup of NW waves covers RUN = 64*NW consecutive
-// pixels; per 16-slot group every wave drops its 16 x 64 range-reduced
-// phases (fp64 reduction to [-pi, pi], then float -- exactly the value the
-// fp32 sincos of the register-tile kernel sees) into LDS, and after one
+// pixels; per 16-slot group every wave drops its 16 x 64 reduced phases
+// (rev_reduce: fp32 revolutions, exactly the value the register-tile
+// kernel feeds to v_sin / v_cos) into LDS, and after one
 // barrier wave w takes slots w*16/NW.. and, per slot, sweeps the RUN pixels
 // plane by plane: RUN*4 contiguous bytes per (slot, plane) instead of 256 B.
 // The LDS tile is double-buffered, so one barrier per group suffices (a
@@ -376,7 +421,8 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
   using L = EvalLds<NW, TPW>;
   __shared__ float tile[2][16][L::kStride];
   const int l = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
+  // wave index, wave-uniform: keeps slot / ring arithmetic on the SALU
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t n_blocks = n_pb * n_sc;
   for (int64_t bb = blockIdx.x; bb < n_blocks; bb += gridDim.x) {
     int64_t pb, sc;
@@ -406,14 +452,7 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
       float(*buf)[L::kStride] = tile[g & 1];
       // ---- contraction: 16 slots x this wave's 64 pixels
       double af[KS];
-      {
-        const int64_t s = s0 + (l & 15);
-#pragma unroll
-        for (int kk = 0; kk < KS; ++kk) {
-          const int d = 4 * kk + (l >> 4);
-          af[kk] = (s < S && d < D) ? coef[s * D + d] : 0.0;
-        }
-      }
+      load_coef<KS>(af, coef, s0, S, D, l, kInv2Pi);
       v4d acc[TPW];
 #pragma unroll
       for (int t = 0; t < TPW; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
@@ -427,13 +466,7 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
       for (int r = 0; r < 4; ++r) {
         float red[TPW];
 #pragma unroll
-        for (int t = 0; t < TPW; ++t) {
-          const double ph = acc[t][r];
-          const double k = rint(ph * 0.15915494309189535);
-          double x = fma(-k, 6.283185307179586, ph);
-          x = fma(-k, 2.4492935982947064e-16, x);
-          red[t] = (float)x;
-        }
+        for (int t = 0; t < TPW; ++t) red[t] = rev_reduce(acc[t][r], scrub);
         float* dst = &buf[acc_row(l, r)][wblk * kWavePix + (l & 15) * kTiles + t0];
         if (TPW == 4)
           *reinterpret_cast<v4f*>(dst) = v4f{red[0], red[1], red[2 % TPW], red[3 % TPW]};
@@ -443,11 +476,12 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
       for (int z = 0; z < sleep; ++z) __builtin_amdgcn_s_sleep(1);
       __syncthreads();
       // ---- stores: wave w owns kSlotsPerWave slots of the group
-#pragma unroll
-      for (int j = 0; j < L::kSlotsPerWave; ++j) {
+      // BE (FITS byte order) as a compile-time branch of a whole slot
+      auto slot_out = [&](int j, auto be_tag) {
+        constexpr bool kBE = decltype(be_tag)::value;
         const int row = w * L::kSlotsPerWave + j;
         const int64_t s = s0 + row;
-        if (s >= S) break;
+        if (s >= S) return;  // uniform per wave
         float cv[L::kChunks][4], sv[L::kChunks][4];
 #pragma unroll
         for (int c = 0; c < L::kChunks; ++c) {
@@ -455,10 +489,8 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             float sn, cs;
-            sincos_reduced(rv[e], sn, cs);
-            if (scrub && isnan(cs)) cs = 1.0f;
-            if (scrub && isnan(sn)) sn = 0.0f;
-            if (be) {
+            sincos_rev(rv[e], sn, cs);
+            if (kBE) {
               cs = bswapf(cs);
               sn = bswapf(sn);
             }
@@ -466,7 +498,9 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
             sv[c][e] = sn;
           }
         }
-        float* o = out + ((s % ring) * 4) * P + pix0 + 4 * l;
+        // S, ring < 2^31 (launch_eval): 32-bit scalar modulo
+        const int64_t so = (uint32_t)s % (uint32_t)ring;
+        float* o = out + (so * 4) * P + pix0 + 4 * l;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
 #pragma unroll
@@ -494,6 +528,13 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
                                (unsigned)__builtin_amdgcn_readlane((int)cs, 48);
           if (l == 0) atomicAdd(sums + s, tot);
         }
+      };
+      if (be) {
+#pragma unroll
+        for (int j = 0; j < L::kSlotsPerWave; ++j) slot_out(j, std::true_type{});
+      } else {
+#pragma unroll
+        for (int j = 0; j < L::kSlotsPerWave; ++j) slot_out(j, std::false_type{});
       }
     }
     // the next workgroup item reuses the LDS tiles from buffer 0
@@ -691,6 +732,13 @@ static int launch_eval_pick(sf_ctx* ctx, const double* coef, const double* cxx,
 int launch_eval(sf_ctx* ctx, const double* coef, const double* cxx,
                 const double* cyy, int64_t S, float* out, int64_t ring,
                 unsigned flags, unsigned* sums) {
+  // the kernels keep slot and ring indices in 32 bits; a ring longer than
+  // the launch changes nothing (slot s -> ring entry s % ring = s)
+  if (S > INT32_MAX) {
+    set_error("sf_kl_eval: more than 2^31 - 1 slots in one call");
+    return SF_EINVAL;
+  }
+  if (ring > S) ring = S > 0 ? S : 1;
   // zero k-step padding (SF_OPT_EVAL_KS_PAD) only for the LDS-staged
   // kernels, which take the real k-step count for their Cpix indexing
   const int v = pick_eval_kernel(ctx, cxx != nullptr, flags,

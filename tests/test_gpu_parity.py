@@ -221,13 +221,19 @@ def test_eval_vs_oracle_sizes(ctx, dev, n_dir, grid):
     np.testing.assert_allclose(out.reshape(want.shape), want, rtol=0, atol=1e-6)
 
 
-def test_eval_ring_and_nan_scrub(ctx, dev):
+@pytest.mark.parametrize("R", [13, 16, 21])
+@pytest.mark.parametrize("fast", [False, True])
+def test_eval_ring_and_nan_scrub(ctx, dev, R, fast):
+    """Ring smaller than the slot count (the per-group ring offset with one
+    wrap when R >= 16, the modulo when R < 16), NaN scrub on and off."""
+    from ska_sdp_screen_fitting_amd._lib import SF_EVAL_FAST_SINCOS
     g = load_golden("synth20")
     coef = g["coef"].reshape(-1, g["coef"].shape[-1])[:50].copy()
     coef[7, 3] = np.nan
-    R = 16
-    out = gpu_eval(ctx, dev, g["piercepoints"], g["x17"], g["y17"], coef, ring=R)
-    full = gpu_eval(ctx, dev, g["piercepoints"], g["x17"], g["y17"], coef)
+    fl = 1 | (SF_EVAL_FAST_SINCOS if fast else 0)
+    out = gpu_eval(ctx, dev, g["piercepoints"], g["x17"], g["y17"], coef, ring=R,
+                   flags=fl)
+    full = gpu_eval(ctx, dev, g["piercepoints"], g["x17"], g["y17"], coef, flags=fl)
     assert np.all(full[7, 0] == 1.0) and np.all(full[7, 1] == 0.0)
     # every value of a ring entry comes from one of the slots that map to it
     # (which one is unspecified: aliasing slots are stored concurrently, so
@@ -236,7 +242,8 @@ def test_eval_ring_and_nan_scrub(ctx, dev):
         cands = np.stack([full[s] for s in range(r, 50, R)])
         assert np.all(np.any(cands == out[r][None], axis=0)), r
     # without the scrub flag NaNs stay NaNs
-    raw = gpu_eval(ctx, dev, g["piercepoints"], g["x17"], g["y17"], coef, flags=0)
+    raw = gpu_eval(ctx, dev, g["piercepoints"], g["x17"], g["y17"], coef,
+                   flags=fl & ~1)
     assert np.all(np.isnan(raw[7]))
 
 
@@ -325,7 +332,9 @@ def test_eval_kernels_agree(ctx, dev, n_dir, grid):
                                 cell, mra, mdec)
     rng = np.random.default_rng(n_dir + grid)
     coef = rng.normal(0, 0.01, size=(45, n_dir))
+    coef[20:30] *= 300.0  # phases of many turns: the range reduction
     coef[9, n_dir // 2] = np.nan
+    coef[31, 0] = np.inf
     base = 1 | SF_EVAL_FAST_SINCOS
     outs = {}
     try:
@@ -350,6 +359,11 @@ def test_eval_kernels_agree(ctx, dev, n_dir, grid):
             ctx.set_option(SF_OPT_EVAL_KS_PAD, 2)
             outs[(kv, "pad")] = gpu_eval(ctx, dev, pp, x, y, coef, flags=base)
             ctx.set_option(SF_OPT_EVAL_KS_PAD, 0)
+            # no NaN scrub: NaN / Inf slots stay NaN in every plane
+            o = gpu_eval(ctx, dev, pp, x, y, coef, flags=SF_EVAL_FAST_SINCOS)
+            assert np.isnan(o[[9, 31]]).all(), kv
+            o[[9, 31]] = 0
+            outs[(kv, "noscrub")] = o
     finally:
         ctx.set_option(SF_OPT_EVAL_KERNEL, SF_EVAL_KERNEL_AUTO)
         ctx.set_option(SF_OPT_EVAL_MAX_BLOCKS, 0)
@@ -357,8 +371,14 @@ def test_eval_kernels_agree(ctx, dev, n_dir, grid):
         ctx.set_option(SF_OPT_EVAL_KS_PAD, 0)
     ref = outs[(SF_EVAL_KERNEL_TILE, 0)]
     for k, o in outs.items():
-        assert np.array_equal(o.view(np.int32), ref.view(np.int32)), k
-    assert np.all(ref[9, 0] == 1.0) and np.all(ref[9, 1] == 0.0)
+        if k[1] == "noscrub":
+            o2 = o.copy()
+            o2[[9, 31]] = ref[[9, 31]]
+            assert np.array_equal(o2.view(np.int32), ref.view(np.int32)), k
+        else:
+            assert np.array_equal(o.view(np.int32), ref.view(np.int32)), k
+    for k in (9, 31):
+        assert np.all(ref[k, 0::2] == 1.0) and np.all(ref[k, 1::2] == 0.0)
     cpix = okl.cpix_matrix(pp, x, y)
     good = np.isfinite(coef).all(axis=1)
     want = okl.eval_planes(okl.eval_phase_screens(coef[good], cpix))

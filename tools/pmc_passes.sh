@@ -1,0 +1,21 @@
+#!/bin/bash
+# Separate rocprofv3 --pmc passes (one run per counter set, per
+# MI355X_MICROARCH.md "rocprofv3 PMC slots": <= 8 SQ, <= 4 TCC, <= 2 GRBM)
+# over one command; CSVs land in OUTDIR/<set>/.
+#   tools/pmc_passes.sh OUTDIR "SETS" -- python3 tools/eval_variants.py ...
+# SETS: any of occ mfma valu lds write fetch
+set -e
+out=$1; sets=$2; shift 3
+export TMPDIR=/tmp
+declare -A C
+C[occ]="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM GRBM_GUI_ACTIVE GRBM_COUNT"
+C[mfma]="SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_INSTS_VALU_MFMA_F64 SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE"
+C[valu]="SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_TRANS_F32 GRBM_GUI_ACTIVE"
+C[lds]="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INST_CYCLES_VMEM_WR SQ_VMEM_WR_TA_DATA_FIFO_FULL SQ_VMEM_TA_CMD_FIFO_FULL SQ_VALU_MFMA_COEXEC_CYCLES SQ_INSTS_VALU_CVT SQ_INSTS_VALU_INT32 GRBM_GUI_ACTIVE"
+C[write]="WRITE_SIZE"
+C[fetch]="FETCH_SIZE"
+for s in $sets; do
+  mkdir -p "$out/$s"
+  timeout -s KILL 150 rocprofv3 --pmc ${C[$s]} -f csv -d "$out/$s" -o p -- "$@" > "$out/$s/run.log" 2>&1
+  echo "pass $s done"
+done
