@@ -686,18 +686,16 @@ int pick_eval_kernel(const sf_ctx* ctx, bool gain, unsigned flags,
   if (opt == SF_EVAL_KERNEL_TILE || opt == SF_EVAL_KERNEL_TILE3) return opt;
   if (!lds_ok) return SF_EVAL_KERNEL_TILE;
   if (opt != SF_EVAL_KERNEL_AUTO) return opt;
-  // measured on MI355X (tools/eval_variants.py, profiles/round1d_eval_variants.txt):
-  // long store runs win while the contraction is light; from ksteps 8 on
-  // (D > 28) the per-group barrier serialises MFMA and stores and the
-  // register-tile kernel is faster, at 3 waves per SIMD from ksteps 10 on
-  // (D > 36: the Cpix fragments alone take 8*ksteps VGPRs); from ksteps 12
-  // on (D > 44) the tile with its Cpix shared in LDS (96 VGPRs, 5 waves/SIMD
-  // at D = 50) beats it: +3-5 % at D = 50, -2 % at D = 40 (512^2;
-  // profiles/round1h_eval_shb.txt)
-  if (ctx->ksteps <= 2) return SF_EVAL_KERNEL_LDS4;
-  if (ctx->ksteps <= 7) return SF_EVAL_KERNEL_LDS16;
-  if (ctx->ksteps <= 9) return SF_EVAL_KERNEL_TILE;
-  return ctx->ksteps <= 11 ? SF_EVAL_KERNEL_TILE3 : SF_EVAL_KERNEL_SHB;
+  // measured on MI355X with the v_sin / v_cos epilogue (tools/eval_variants.py,
+  // profiles/round2c_eval_sweep.txt): the LDS-staged kernels' long store runs
+  // win up to D = 44 (16 waves up to D = 32, 4 waves / 1 KiB runs beyond,
+  // where the 16-wave barrier starts to serialise MFMA and stores; 16 waves
+  // with half tiles for D <= 12); from D = 45 the register tile (2 waves /
+  // SIMD, Cpix fragments in registers) is 4-10 % ahead of every LDS shape
+  if (ctx->ksteps <= 3) return SF_EVAL_KERNEL_LDS16H;
+  if (ctx->ksteps <= 8) return SF_EVAL_KERNEL_LDS16;
+  if (ctx->ksteps <= 11) return SF_EVAL_KERNEL_LDS4;
+  return SF_EVAL_KERNEL_TILE;
 }
 
 template <int KS>
