@@ -128,6 +128,10 @@ int sf_device_cus(sf_ctx* ctx, int* n_cu);
  * blocks pb = x (mod 8); -1 (default): 1 when an XCD's eighth is at most 8
  * pixel blocks (256^2 with 4 KiB runs: +2-3 % measured), else 0. */
 #define SF_OPT_EVAL_XCD_MAP 7
+/* SF_OPT_EVAL_GROUPS = g (1..256, power of two; 0 = auto = 256): most
+ * 16-slot groups per evaluation work item (each item loads its pixel block's
+ * basis once, so longer items re-read less of it). */
+#define SF_OPT_EVAL_GROUPS 8
 #define SF_EVAL_KERNEL_AUTO 0
 #define SF_EVAL_KERNEL_TILE 1
 #define SF_EVAL_KERNEL_LDS4 2
@@ -230,12 +234,29 @@ int sf_kl_eval_sums(sf_ctx* ctx, const double* coef_phase,
  * (voronoi_screen.py:132-216, screen.py:353-362).  Device inputs: labels
  * [ny][nx] int32 in 1..D (the template of make_rasertize_template), phase
  * [S][D] float64 (already referenced), amp_xx / amp_yy [S][D] float64 or NULL
- * (phase-only: amplitude 1).  Output as sf_kl_eval.  smooth_pix <= 6.
+ * (phase-only: amplitude 1).  Output as sf_kl_eval.  smooth_pix <= 6 runs
+ * fused in one LDS-tiled kernel; larger values (any sigma, as scipy) gather
+ * first and then run the passes of sf_smooth, which needs ring_slots >= S.
+ * A label outside 1..D (the template never makes one) gives NaN pixels (1 / 0
+ * under SF_EVAL_NAN_SCRUB); no table entry is read for it.
  */
 int sf_tess_fill(sf_ctx* ctx, const int32_t* labels, int nx, int ny,
                  const double* phase, const double* amp_xx,
                  const double* amp_yy, int D, int64_t S, float* out,
                  int64_t ring_slots, double smooth_pix, unsigned flags);
+
+/*
+ * The Gaussian smoothing of Screen.write (screen.py:353-362:
+ * scipy.ndimage.gaussian_filter(., sigma=(0, smooth_pix, smooth_pix)) per
+ * image, float32 between the y and x passes, 'reflect' borders, truncate
+ * 4 sigma) in place on n_img images [n_img][ny][nx] float32 on the device --
+ * the cube [S][4][ny][nx] is n_img = 4 S images (n_img must be a multiple of
+ * 4).  SF_EVAL_NAN_SCRUB / SF_EVAL_BIG_ENDIAN in flags apply after smoothing,
+ * as the reference scrubs after smoothing: evaluate without them, then
+ * smooth with them.  Any smooth_pix (device pass buffer <= 256 MiB).
+ */
+int sf_smooth(sf_ctx* ctx, float* cube, int nx, int ny, int64_t n_img,
+              double smooth_pix, unsigned flags);
 
 #ifdef __cplusplus
 }

@@ -100,6 +100,7 @@ int sf_destroy(sf_ctx* ctx) {
   hipFree(ctx->d_wscratch);
   hipFree(ctx->d_oscratch);
   hipFree(ctx->d_gw);
+  hipFree(ctx->d_smooth);
   delete ctx;
   return SF_OK;
 }
@@ -177,6 +178,11 @@ int sf_set_option(sf_ctx* ctx, int option, int value) {
       SF_REQUIRE(value >= -1 && value <= 1, SF_EINVAL,
                  "sf_set_option: XCD map must be -1, 0 or 1");
       ctx->eval_xcd_map = value;
+      return SF_OK;
+    case SF_OPT_EVAL_GROUPS:
+      SF_REQUIRE(value >= 0 && value <= 256 && (value & (value - 1)) == 0,
+                 SF_EINVAL, "sf_set_option: groups must be 0 or a power of two <= 256");
+      ctx->eval_groups = value;
       return SF_OK;
     case SF_OPT_EVAL_MAX_BLOCKS:
       SF_REQUIRE(value >= 0, SF_EINVAL, "sf_set_option: negative block cap");
@@ -427,6 +433,41 @@ int sf_kl_eval_sums(sf_ctx* ctx, const double* coef_phase,
                          reinterpret_cast<unsigned*>(slot_sums));
 }
 
+// scipy.ndimage._gaussian_kernel1d(sigma, 0, int(4 sigma + 0.5)) uploaded to
+// ctx->d_gw (stream-ordered); R = 0 for sigma <= 1e-15
+static int upload_gaussian(sf_ctx* ctx, double sigma, int* R_out) {
+  int R = 0;
+  std::vector<double> w(1, 1.0);
+  if (sigma > 1e-15) {
+    R = (int)(4.0 * sigma + 0.5);
+    w.assign(2 * R + 1, 0.0);
+    double sum = 0.0;
+    for (int i = -R; i <= R; ++i)
+      w[i + R] = std::exp(-0.5 / (sigma * sigma) * (double)(i * i));
+    for (int i = 0; i < 2 * R + 1; ++i) sum += w[i];
+    for (int i = 0; i < 2 * R + 1; ++i) w[i] /= sum;
+  }
+  if (ctx->gw_cap < w.size()) {
+    if (ctx->d_gw) (void)hipFree(ctx->d_gw);
+    ctx->d_gw = nullptr;
+    ctx->gw_cap = 0;
+    const size_t cap = w.size() < 64 ? 64 : w.size();
+    if (hipMalloc(reinterpret_cast<void**>(&ctx->d_gw), cap * sizeof(double)) !=
+        hipSuccess) {
+      set_error("hipMalloc failed");
+      return SF_ENOMEM;
+    }
+    ctx->gw_cap = cap;
+  }
+  // a synchronous copy: the host vector dies here and an earlier launch on
+  // the stream may still read the previous weights
+  SF_HIP(hipStreamSynchronize(ctx->stream));
+  SF_HIP(hipMemcpy(ctx->d_gw, w.data(), w.size() * sizeof(double),
+                   hipMemcpyHostToDevice));
+  *R_out = R;
+  return SF_OK;
+}
+
 int sf_tess_fill(sf_ctx* ctx, const int32_t* labels, int nx, int ny,
                  const double* phase, const double* amp_xx,
                  const double* amp_yy, int D, int64_t S, float* out,
@@ -434,34 +475,41 @@ int sf_tess_fill(sf_ctx* ctx, const int32_t* labels, int nx, int ny,
   SF_REQUIRE(ctx && labels && phase && out, SF_EINVAL, "sf_tess_fill: NULL argument");
   SF_REQUIRE(nx >= 1 && ny >= 1 && D >= 1 && D <= 64 && S >= 0 && ring >= 1,
              SF_EINVAL, "sf_tess_fill: bad shape");
-  SF_REQUIRE(smooth_pix >= 0.0 && smooth_pix <= 6.0, SF_EINVAL,
-             "sf_tess_fill: smooth_pix must be in [0, 6]");
+  SF_REQUIRE(smooth_pix >= 0.0 && smooth_pix <= 1e4, SF_EINVAL,
+             "sf_tess_fill: smooth_pix must be in [0, 1e4]");
   if (S == 0) return SF_OK;
   SF_HIP(hipSetDevice(ctx->device));
-  // scipy.ndimage._gaussian_kernel1d(sigma, 0, int(4 sigma + 0.5))
   int R = 0;
-  std::vector<double> w(1, 1.0);
-  if (smooth_pix > 1e-15) {
-    R = (int)(4.0 * smooth_pix + 0.5);
-    w.assign(2 * R + 1, 0.0);
-    double sum = 0.0;
-    for (int i = -R; i <= R; ++i) {
-      w[i + R] = std::exp(-0.5 / (smooth_pix * smooth_pix) * (double)(i * i));
-    }
-    for (int i = 0; i < 2 * R + 1; ++i) sum += w[i];
-    for (int i = 0; i < 2 * R + 1; ++i) w[i] /= sum;
-  }
-  if (!ctx->d_gw) {
-    if (hipMalloc(reinterpret_cast<void**>(&ctx->d_gw), 64 * sizeof(double)) !=
-        hipSuccess) {
-      set_error("hipMalloc failed");
-      return SF_ENOMEM;
-    }
-  }
-  SF_HIP(hipMemcpyAsync(ctx->d_gw, w.data(), w.size() * sizeof(double),
-                        hipMemcpyHostToDevice, ctx->stream));
-  return sf::launch_tess(ctx, labels, nx, ny, phase, amp_xx, amp_yy, D, S,
-                         out, ring, ctx->d_gw, R, flags);
+  int rc = upload_gaussian(ctx, smooth_pix, &R);
+  if (rc != SF_OK) return rc;
+  if (R <= sf::kTessMaxR)
+    return sf::launch_tess(ctx, labels, nx, ny, phase, amp_xx, amp_yy, D, S,
+                           out, ring, ctx->d_gw, R, flags);
+  // wider Gaussians: gather unsmoothed and unscrubbed, then the separable
+  // passes of sf_smooth (scrub / byte swap after smoothing, as the
+  // reference); every slot needs its own cube for that
+  SF_REQUIRE(ring >= S, SF_EINVAL,
+             "sf_tess_fill: smooth_pix > 6 needs ring_slots >= S");
+  rc = sf::launch_tess(ctx, labels, nx, ny, phase, amp_xx, amp_yy, D, S, out,
+                       ring, ctx->d_gw, 0, 0u);
+  if (rc != SF_OK) return rc;
+  return sf::launch_smooth(ctx, out, nx, ny, S * 4, ctx->d_gw, R, flags);
+}
+
+int sf_smooth(sf_ctx* ctx, float* cube, int nx, int ny, int64_t n_img,
+              double smooth_pix, unsigned flags) {
+  SF_REQUIRE(ctx && cube && nx >= 1 && ny >= 1 && n_img >= 0, SF_EINVAL,
+             "sf_smooth: bad argument");
+  SF_REQUIRE(n_img % 4 == 0, SF_EINVAL,
+             "sf_smooth: n_img must count whole [4][ny][nx] slot cubes");
+  SF_REQUIRE(smooth_pix >= 0.0 && smooth_pix <= 1e4, SF_EINVAL,
+             "sf_smooth: smooth_pix must be in [0, 1e4]");
+  if (n_img == 0) return SF_OK;
+  SF_HIP(hipSetDevice(ctx->device));
+  int R = 0;
+  const int rc = upload_gaussian(ctx, smooth_pix, &R);
+  if (rc != SF_OK) return rc;
+  return sf::launch_smooth(ctx, cube, nx, ny, n_img, ctx->d_gw, R, flags);
 }
 
 }  // extern "C"

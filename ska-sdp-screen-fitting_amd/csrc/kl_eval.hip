@@ -556,6 +556,21 @@ static int64_t eval_grid(const sf_ctx* ctx, int64_t n_pb, int64_t n_sc,
   return n < cap ? n : cap;
 }
 
+// 16-slot groups per (pixel block, slot chunk) work item: as many as keep
+// >= min_items items (the grid fills the chip), at most max_groups.  Every
+// item loads its pixel block's Cpix fragments once, so long chunks keep that
+// reload small against the item's output: at 512^2 x D = 50 the Cpix of one
+// XCD's pixel blocks (13.6 MB) outgrows its 4 MiB L2, and 16 groups per item
+// re-read 3.6 TB of it per 8.2 M-slot launch (FETCH_SIZE, 10 % of the
+// writes); 256 groups (4096 slots) cut that 16x.
+static int eval_chunk_groups(int64_t n_pb, int64_t S, int max_groups,
+                             int64_t min_items) {
+  int groups = max_groups;
+  while (groups > 1 && n_pb * ((S + 16 * groups - 1) / (16 * groups)) < min_items)
+    groups >>= 1;
+  return groups;
+}
+
 int launch_cpix(sf_ctx* ctx, const double* d_x, const double* d_y) {
   const int64_t n_wpb = ctx->n_pix_blocks * kEvalWaves;
   const int64_t n = n_wpb * ctx->ksteps * kTiles * 64;
@@ -574,11 +589,7 @@ static int launch_eval_ks(sf_ctx* ctx, const double* coef,
                           unsigned* sums) {
   const int64_t P = ctx->n_pix;
   const int64_t n_pb = ctx->n_pix_blocks;
-  // slot chunk per workgroup: 16 groups of 16 slots (1 MiB of output at
-  // 256 pixels), fewer when S is small so the grid still fills 256 CUs
-  int groups = 16;
-  while (groups > 1 && n_pb * ((S + 16 * groups - 1) / (16 * groups)) < 2048)
-    groups >>= 1;
+  const int groups = eval_chunk_groups(n_pb, S, ctx->eval_groups ? ctx->eval_groups : 256, 2048);
   const int64_t n_sc = (S + 16 * groups - 1) / (16 * groups);
   const int64_t nblk = eval_grid(ctx, n_pb, n_sc, 256);
   const bool vec4 = (P % 4 == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
@@ -619,9 +630,7 @@ static int launch_eval_shb(sf_ctx* ctx, const double* coef, int64_t S,
                            unsigned* sums) {
   const int64_t P = ctx->n_pix;
   const int64_t n_wpb = ctx->n_pix_blocks * kEvalWaves;
-  int groups = 64;
-  while (groups > 4 && n_wpb * ((S + 16 * groups - 1) / (16 * groups)) < 4096)
-    groups >>= 1;
+  const int groups = eval_chunk_groups(n_wpb, S, ctx->eval_groups ? ctx->eval_groups : 256, 4096);
   const int64_t n_sc = (S + 16 * groups - 1) / (16 * groups);
   const int64_t nblk = eval_grid(ctx, n_wpb, n_sc, 256);
   const bool fast = flags & SF_EVAL_FAST_SINCOS;
@@ -648,9 +657,7 @@ static int launch_eval_lds(sf_ctx* ctx, const double* coef, int64_t S,
   const int64_t P = ctx->n_pix;
   const int64_t run = EvalLds<NW, TPW>::kRun;
   const int64_t n_pb = (P + run - 1) / run;
-  int groups = 16;
-  while (groups > 1 && n_pb * ((S + 16 * groups - 1) / (16 * groups)) < 1024)
-    groups >>= 1;
+  const int groups = eval_chunk_groups(n_pb, S, ctx->eval_groups ? ctx->eval_groups : 256, 1024);
   const int64_t n_sc = (S + 16 * groups - 1) / (16 * groups);
   const int64_t nblk = eval_grid(ctx, n_pb, n_sc, 64 * NW);
   // auto XCD map: interleave the pixel blocks over the XCDs when each XCD's

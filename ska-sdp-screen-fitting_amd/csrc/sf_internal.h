@@ -79,8 +79,11 @@ struct sf_ctx {
   size_t scratch_cap = 0;
   float* d_wscratch = nullptr;
   int32_t* d_oscratch = nullptr;
-  // Gaussian weights of sf_tess_fill
+  // Gaussian weights of sf_tess_fill / sf_smooth, pass buffer of sf_smooth
   double* d_gw = nullptr;
+  size_t gw_cap = 0;                     // doubles
+  float* d_smooth = nullptr;
+  size_t smooth_cap = 0;                 // bytes
   // fast-path switch (SCREENFIT_FIT=general forces the general kernel)
   int force_general = 0;
   // evaluation kernel (SF_OPT_EVAL_KERNEL)
@@ -89,6 +92,7 @@ struct sf_ctx {
   int eval_ks_pad = 0;          // SF_OPT_EVAL_KS_PAD: extra zero k-steps
   int eval_sleep = 0;           // SF_OPT_EVAL_SLEEP: x 64 cycles per group
   int eval_xcd_map = -1;        // SF_OPT_EVAL_XCD_MAP (-1 = auto)
+  int eval_groups = 0;          // SF_OPT_EVAL_GROUPS (0 = auto = 256)
   int fit_pack = 1;             // SF_OPT_FIT_PACK: 2 slots per wave for D <= 32
 };
 
@@ -120,4 +124,7 @@ int launch_tess(sf_ctx* ctx, const int32_t* labels, int nx, int ny,
                 const double* phase, const double* amp_xx,
                 const double* amp_yy, int D, int64_t S, float* out,
                 int64_t ring, const double* d_w, int R, unsigned flags);
+int launch_smooth(sf_ctx* ctx, float* cube, int nx, int ny, int64_t n_img,
+                  const double* d_w, int R, unsigned flags);
+constexpr int kTessMaxR = 24;  // Gaussian radius of the fused tess kernel
 }  // namespace sf

@@ -28,6 +28,7 @@ SF_OPT_FIT_PACK = 4
 SF_OPT_EVAL_KS_PAD = 5
 SF_OPT_EVAL_SLEEP = 6
 SF_OPT_EVAL_XCD_MAP = 7
+SF_OPT_EVAL_GROUPS = 8
 SF_EVAL_KERNEL_AUTO = 0
 SF_EVAL_KERNEL_TILE = 1
 SF_EVAL_KERNEL_LDS4 = 2
@@ -53,7 +54,7 @@ EXPORTED = (
     "sf_set_basis", "sf_get_basis", "sf_kl_fit", "sf_get_fit_stats",
     "sf_stream_create", "sf_stream_destroy", "sf_device_cus",
     "sf_set_grid", "sf_kl_eval", "sf_kl_eval_gain", "sf_kl_eval_sums",
-    "sf_tess_fill",
+    "sf_tess_fill", "sf_smooth",
 )
 
 
@@ -118,6 +119,7 @@ def load_library(path=None):
                                 c_int),
             "sf_tess_fill": ([vp, vp, c_int, c_int, vp, vp, vp, c_int, i64, vp,
                               i64, c_dbl, ctypes.c_uint], c_int),
+            "sf_smooth": ([vp, vp, c_int, c_int, i64, c_dbl, ctypes.c_uint], c_int),
         }
         for name, (args, res) in sig.items():
             fn = getattr(lib, name)
@@ -138,17 +140,21 @@ _TORCH_DTYPES = {np.float64: "torch.float64", np.float32: "torch.float32",
                  np.int32: "torch.int32", np.int64: "torch.int64"}
 
 
-def _dev(x, dtype, numel, name):
+def _dev(x, dtype, numel, name, device=None):
     """Pointer of a device operand after checking what the kernels assume:
-    a contiguous CUDA tensor of ``dtype`` with at least ``numel`` elements
-    (a short or mistyped buffer would be overrun on the GPU).  Raw integer
-    pointers are the caller's responsibility."""
+    a contiguous CUDA tensor of ``dtype`` with at least ``numel`` elements on
+    the context's ``device`` (a short, mistyped or foreign-device buffer would
+    be overrun or dereferenced by the wrong GPU).  Raw integer pointers are
+    the caller's responsibility."""
     if x is None or isinstance(x, int):
         return x
     if not hasattr(x, "data_ptr"):
         raise TypeError(f"{name}: expected a device tensor, got {type(x).__name__}")
     if not x.is_cuda:
         raise ValueError(f"{name}: must be a device (cuda) tensor")
+    if device is not None and x.device.index != device:
+        raise ValueError(f"{name}: on cuda:{x.device.index}, the context is on "
+                         f"cuda:{device}")
     if str(x.dtype) != _TORCH_DTYPES[dtype]:
         raise TypeError(f"{name}: dtype {x.dtype}, expected {_TORCH_DTYPES[dtype]}")
     if not x.is_contiguous():
@@ -180,6 +186,9 @@ class Context:
             self.close()
         except Exception:
             pass
+
+    def _dev(self, x, dtype, numel, name):
+        return _dev(x, dtype, numel, name, self.device)
 
     def set_stream(self, stream_handle):
         _check(self.lib.sf_set_stream(self.h, stream_handle), "sf_set_stream")
@@ -226,16 +235,16 @@ class Context:
         n = int(T) * int(F) * int(A) * self.D
         prm = FitParams(int(screen_type), int(niter), float(nsigma),
                         int(bool(adjust_order)), int(ref_ant), int(ant_offset),
-                        _dev(ref_phase, np.float64, int(T) * int(F) * self.D,
+                        self._dev(ref_phase, np.float64, int(T) * int(F) * self.D,
                              "ref_phase"))
         _check(self.lib.sf_kl_fit(
-            self.h, _dev(phase, np.float64, n, "phase"),
-            _dev(weight, np.float32, n, "weight"), int(T), int(F), int(A),
+            self.h, self._dev(phase, np.float64, n, "phase"),
+            self._dev(weight, np.float32, n, "weight"), int(T), int(F), int(A),
             so.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
-            ctypes.byref(prm), _dev(coef, np.float64, n, "coef"),
-            _dev(resid, np.float64, n, "resid"),
-            _dev(w_out, np.float32, n, "w_out"),
-            _dev(order_out, np.int32, n // max(self.D, 1), "order_out")),
+            ctypes.byref(prm), self._dev(coef, np.float64, n, "coef"),
+            self._dev(resid, np.float64, n, "resid"),
+            self._dev(w_out, np.float32, n, "w_out"),
+            self._dev(order_out, np.int32, n // max(self.D, 1), "order_out")),
             "sf_kl_fit")
 
     def fit_stats(self):
@@ -259,8 +268,8 @@ class Context:
              flags=SF_EVAL_NAN_SCRUB | SF_EVAL_FAST_SINCOS | SF_EVAL_NT_STORES):
         ring = max(int(S if ring_slots is None else ring_slots), 1)
         _check(self.lib.sf_kl_eval(
-            self.h, _dev(coef, np.float64, int(S) * self.D, "coef"), int(S),
-            _dev(out, np.float32, self._out_numel(S, ring), "out"), ring,
+            self.h, self._dev(coef, np.float64, int(S) * self.D, "coef"), int(S),
+            self._dev(out, np.float32, self._out_numel(S, ring), "out"), ring,
             int(flags)), "sf_kl_eval")
 
 
@@ -287,10 +296,10 @@ class Context:
         ring = max(int(S if ring_slots is None else ring_slots), 1)
         n = int(S) * self.D
         _check(self.lib.sf_kl_eval_gain(
-            self.h, _dev(coef_ph, np.float64, n, "coef_ph"),
-            _dev(coef_xx, np.float64, n, "coef_xx"),
-            _dev(coef_yy, np.float64, n, "coef_yy"), int(S),
-            _dev(out, np.float32, self._out_numel(S, ring), "out"), ring,
+            self.h, self._dev(coef_ph, np.float64, n, "coef_ph"),
+            self._dev(coef_xx, np.float64, n, "coef_xx"),
+            self._dev(coef_yy, np.float64, n, "coef_yy"), int(S),
+            self._dev(out, np.float32, self._out_numel(S, ring), "out"), ring,
             int(flags)), "sf_kl_eval_gain")
 
     def eval_sums(self, coef, S, out, sums, ring_slots=None, coef_xx=None,
@@ -303,24 +312,37 @@ class Context:
         ring = max(int(S if ring_slots is None else ring_slots), 1)
         n = int(S) * self.D
         _check(self.lib.sf_kl_eval_sums(
-            self.h, _dev(coef, np.float64, n, "coef"),
-            _dev(coef_xx, np.float64, n, "coef_xx"),
-            _dev(coef_yy, np.float64, n, "coef_yy"), int(S),
-            _dev(out, np.float32, self._out_numel(S, ring), "out"), ring,
-            int(flags), _dev(sums, np.int32, int(S), "sums")), "sf_kl_eval_sums")
+            self.h, self._dev(coef, np.float64, n, "coef"),
+            self._dev(coef_xx, np.float64, n, "coef_xx"),
+            self._dev(coef_yy, np.float64, n, "coef_yy"), int(S),
+            self._dev(out, np.float32, self._out_numel(S, ring), "out"), ring,
+            int(flags), self._dev(sums, np.int32, int(S), "sums")), "sf_kl_eval_sums")
 
     def tess_fill(self, labels, nx, ny, phase, D, S, out, ring_slots=None,
                   amp_xx=None, amp_yy=None, smooth_pix=0.0,
                   flags=SF_EVAL_NAN_SCRUB):
         ring = max(int(S if ring_slots is None else ring_slots), 1)
         n = int(S) * int(D)
+        if hasattr(labels, "min") and labels.numel():
+            lo, hi = int(labels.min()), int(labels.max())
+            if lo < 1 or hi > int(D):
+                raise ValueError(f"labels: values {lo}..{hi} outside 1..{D}")
         _check(self.lib.sf_tess_fill(
-            self.h, _dev(labels, np.int32, int(nx) * int(ny), "labels"),
-            int(nx), int(ny), _dev(phase, np.float64, n, "phase"),
-            _dev(amp_xx, np.float64, n, "amp_xx"),
-            _dev(amp_yy, np.float64, n, "amp_yy"), int(D), int(S),
-            _dev(out, np.float32, min(int(S), ring) * 4 * int(nx) * int(ny), "out"),
+            self.h, self._dev(labels, np.int32, int(nx) * int(ny), "labels"),
+            int(nx), int(ny), self._dev(phase, np.float64, n, "phase"),
+            self._dev(amp_xx, np.float64, n, "amp_xx"),
+            self._dev(amp_yy, np.float64, n, "amp_yy"), int(D), int(S),
+            self._dev(out, np.float32, min(int(S), ring) * 4 * int(nx) * int(ny), "out"),
             ring, float(smooth_pix), int(flags)), "sf_tess_fill")
+
+
+    def smooth(self, cube, nx, ny, n_img, smooth_pix, flags=0):
+        """sf_smooth: Screen.write's Gaussian in place on n_img float32
+        images [n_img][ny][nx] (n_img = 4 x slots), scrub / byte swap in
+        ``flags`` applied after smoothing."""
+        _check(self.lib.sf_smooth(
+            self.h, self._dev(cube, np.float32, int(n_img) * int(nx) * int(ny), "cube"),
+            int(nx), int(ny), int(n_img), float(smooth_pix), int(flags)), "sf_smooth")
 
 
 _contexts = {}

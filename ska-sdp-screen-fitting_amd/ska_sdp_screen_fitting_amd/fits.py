@@ -112,32 +112,36 @@ class CubeWriter:
         self.fh = None
 
 
-def read_cube(path):
-    """Read back (header dict, data) of a file written by CubeWriter (tests)."""
-    with open(path, "rb") as fh:
-        raw = fh.read()
+def read_cube(path, mmap=False):
+    """Read back (header dict, data) of a file written by CubeWriter (tests);
+    ``mmap``: the data as a read-only big-endian memory map instead of a copy
+    (cubes of several GB)."""
     hdr = {}
     off = 0
-    while True:
-        c = raw[off:off + 80].decode("ascii")
-        off += 80
-        if c.startswith("END"):
-            break
-        if c[8:10] == "= ":
-            k, v = c[:8].strip(), c[10:].strip()
-            if v.startswith("'"):
-                v = v[1:v.rindex("'")].rstrip()
-            elif v in ("T", "F"):
-                v = v == "T"
-            else:
-                try:
-                    v = int(v)
-                except ValueError:
-                    v = float(v)
-            hdr[k] = v
-    off += (-off) % BLOCK
-    n = hdr["NAXIS"]
-    shape = tuple(hdr[f"NAXIS{n - i}"] for i in range(n))
-    count = int(np.prod(shape))
-    data = np.frombuffer(raw, dtype=">f4", count=count, offset=off).reshape(shape)
-    return hdr, data
+    with open(path, "rb") as fh:
+        while True:
+            c = fh.read(80).decode("ascii")
+            off += 80
+            if not c or c.startswith("END"):
+                break
+            if c[8:10] == "= ":
+                k, v = c[:8].strip(), c[10:].strip()
+                if v.startswith("'"):
+                    v = v[1:v.rindex("'")].rstrip()
+                elif v in ("T", "F"):
+                    v = v == "T"
+                else:
+                    try:
+                        v = int(v)
+                    except ValueError:
+                        v = float(v)
+                hdr[k] = v
+        off += (-off) % BLOCK
+        n = hdr["NAXIS"]
+        shape = tuple(hdr[f"NAXIS{n - i}"] for i in range(n))
+        if mmap:
+            return hdr, np.memmap(path, dtype=">f4", mode="r", offset=off, shape=shape)
+        fh.seek(off)
+        count = int(np.prod(shape))
+        data = np.frombuffer(fh.read(4 * count), dtype=">f4", count=count)
+    return hdr, data.reshape(shape)

@@ -2,10 +2,12 @@
 reference).
 
 ``KLScreen`` keeps the reference's constructor and methods.  ``fit`` runs the
-batched GPU fit (``stationscreen.run``); ``make_matrix`` and ``write``
-evaluate the screens with the HIP kernel ``kl_eval_kernel`` (MFMA float64
-contraction + sincos epilogue) instead of a per-pixel Python loop in a
-process pool.
+batched GPU fit (``stationscreen.run`` -> ``sf_kl_fit``: the fit-pass,
+subset-eigenbasis and classify kernels of csrc/kl_fit_fast.hip);
+``make_matrix`` and ``write`` evaluate the screens with ``sf_kl_eval`` (the
+LDS-staged ``kl_eval_lds_kernel`` or the register-tile ``kl_eval_kernel`` of
+csrc/kl_eval.hip, chosen per D: an MFMA float64 contraction + sincos
+epilogue) instead of a per-pixel Python loop in a process pool.
 """
 
 import multiprocessing
@@ -15,12 +17,12 @@ import numpy as np
 from . import geometry
 from . import stationscreen
 from ._lib import (SF_EVAL_BIG_ENDIAN, SF_EVAL_FAST_SINCOS, SF_EVAL_NAN_SCRUB,
-                   SF_EVAL_NT_STORES, get_context)
+                   SF_EVAL_NT_STORES, Context)
 from .h5parm import H5parm, get_reference_station
 from .screen import Screen
 
-# NaN scrub (screen.py:368-378) + fp64 range reduction / fp32 sincos +
-# streaming stores
+# NaN scrub (screen.py:368-378) + exact fp64 reduction of the phase in
+# revolutions / hardware fp32 sincos + streaming stores
 DEFAULT_FLAGS = SF_EVAL_NAN_SCRUB | SF_EVAL_FAST_SINCOS | SF_EVAL_NT_STORES
 
 
@@ -37,14 +39,17 @@ def read_patch_names(skymodel_filename):
 
 
 class KLEvaluator:
-    """Device state for evaluating KL screens on one grid."""
+    """Device state for evaluating KL screens on one grid.  Owns its sf_ctx:
+    the basis and pixel grid it sets stay put whatever other screens or the
+    fit (which uses the process-wide context of ``get_context``) set
+    meanwhile."""
 
     def __init__(self, piercepoints, r_0, beta, x_coord, y_coord, device=0):
         import torch
 
         self.torch = torch
         self.dev = torch.device("cuda", device)
-        self.ctx = get_context(device)
+        self.ctx = Context(device)
         self.pp = np.asarray(piercepoints, np.float64)
         self.D = self.pp.shape[0]
         self.nx, self.ny = len(x_coord), len(y_coord)
@@ -77,6 +82,16 @@ class KLEvaluator:
         with torch.cuda.device(self.dev):
             self.ctx.set_stream(torch.cuda.current_stream(self.dev).cuda_stream)
             self.ctx.eval_gain(coef_dev, xx_dev, yy_dev, S, out_dev, S, flags)
+        return out_dev
+
+    def smooth_device(self, out_dev, smooth_pix, flags):
+        """Screen.write's Gaussian (screen.py:353-362) in place on a device
+        cube [S, 4, ny, nx]; scrub / byte swap in ``flags`` after it."""
+        torch = self.torch
+        with torch.cuda.device(self.dev):
+            self.ctx.set_stream(torch.cuda.current_stream(self.dev).cuda_stream)
+            self.ctx.smooth(out_dev, self.nx, self.ny, 4 * out_dev.shape[0],
+                            smooth_pix, flags)
         return out_dev
 
     def _upload(self, a):
@@ -120,6 +135,7 @@ class KLScreen(Screen):
         with per-station orders referenced to a central station; for gain
         solutions also the XX / YY log10 amplitudes (order
         min(12, max(3, round(D / 2))), 3 iterations, no order scaling)."""
+        self._evaluators = {}  # a refit invalidates the evaluated basis
         h5 = H5parm(self.input_h5parm_filename)
         solset = h5.get_solset(self.input_solset_name)
         soltab_ph = solset.get_soltab(self.input_phase_soltab_name)
@@ -221,12 +237,18 @@ class KLScreen(Screen):
                 s0, s1 = (t0 - g_start) * n_f * n_a, (t1 - g_start) * n_f * n_a
                 slot, buf = pipe.device_buffer((s1 - s0) * per_slot)
                 out = buf.view(torch.float32).view(s1 - s0, 4, ev.ny, ev.nx)
-                flags = DEFAULT_FLAGS | SF_EVAL_BIG_ENDIAN
+                fin = SF_EVAL_NAN_SCRUB | SF_EVAL_BIG_ENDIAN
+                # with smoothing, scrub and byte swap come after the Gaussian
+                # (screen.py:353-378 smooths, then replaces NaNs)
+                flags = DEFAULT_FLAGS | fin if smooth_pix <= 0 else \
+                    DEFAULT_FLAGS & ~SF_EVAL_NAN_SCRUB
                 if self.phase_only:
                     ev.eval_device(coef[s0:s1], out, flags)
                 else:
                     ev.eval_gain_device(coef[s0:s1], c_xx[s0:s1], c_yy[s0:s1],
                                         out, flags)
+                if smooth_pix > 0:
+                    ev.smooth_device(out, smooth_pix, fin)
                 pipe.submit(slot, (s1 - s0) * per_slot, writer)
         finally:
             pipe.close()

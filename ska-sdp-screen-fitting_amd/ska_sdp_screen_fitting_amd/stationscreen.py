@@ -2,8 +2,11 @@
 
 Same signature, argument meaning, return codes and soltab side effects as the
 reference operator (stationscreen.py:858-1161), but every (station, time,
-freq) slot is fitted by the HIP kernel ``kl_fit_kernel`` (one wavefront per
-slot, see csrc/kl_fit.hip) through the C ABI ``sf_kl_fit``.  The host does
+freq) slot is fitted on the GPU through the C ABI ``sf_kl_fit``: the
+classify / mask-assign / subset-eigenbasis kernels and ``kl_fit_pass_kernel``
+of csrc/kl_fit_fast.hip (one slot per wavefront, two per wavefront in 32-lane
+groups for D <= 32; eigenbasis solve), with ``kl_fit_general_kernel``
+(csrc/kl_fit.hip) for slots whose weights sit at the pinv cutoff.  The host does
 only the O(A + D) setup: piercepoints and midpoint, per-station orders, the
 shared basis upload, and the soltab bookkeeping.
 """

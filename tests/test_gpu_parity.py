@@ -293,6 +293,117 @@ def test_make_aterm_image_fixture_kl(tmp_path):
     assert n_in >= 5
 
 
+def test_make_aterm_image_config2_kl128(tmp_path):
+    """BASELINE config 2 end to end: make_aterm_image on the fixture, KL,
+    cellsize 0.02602 deg (a 128^2 grid, 3.9 GB FITS cube): the reference's
+    own evaluated planes at (t 4:6; f, station (3, 7), (9, 44)) within 1e-6,
+    the reference's header cards, and its test criterion at the patch pixels
+    (tests/test_fit_screens.py:131-215, with abs())."""
+    import json
+    from ska_sdp_screen_fitting_amd import fits as sffits
+    from ska_sdp_screen_fitting_amd.geometry import sin_world2pix
+    from ska_sdp_screen_fitting_amd.make_aterm_images import make_aterm_image
+
+    g = load_golden("fixture_kl")
+    outroot = str(tmp_path / "kl128")
+    make_aterm_image(os.path.join(GOLDEN, "fixture_kl.npz"), soltabname="phase000",
+                     screen_type="kl", outroot=outroot,
+                     bounds_deg=[124.565, 66.165, 127.895, 62.835],
+                     bounds_mid_deg=[126.23, 64.50],
+                     skymodel=os.path.join(GOLDEN, "skymodel.txt"),
+                     solsetname="sol000", padding_fraction=0, cellsize_deg=0.02602,
+                     ncpu=0)
+    files = open(str(tmp_path / "kl128.txt")).read().split()
+    assert files == [outroot + "_0.fits"]
+    hdr, cube = sffits.read_cube(outroot + "_0.fits", mmap=True)
+    assert cube.shape == (20, 12, 62, 4, 128, 128)
+    want_hdr = json.load(open(os.path.join(GOLDEN, "fixture_headers.json")))["128"]
+    for k, v in want_hdr:
+        if isinstance(v, float):
+            assert hdr[k] == pytest.approx(v, rel=1e-15), k
+        elif k in ("SIMPLE", "EXTEND"):
+            assert hdr[k] is True
+        else:
+            assert hdr[k] == v, k
+    t0, t1 = g["kl128_t"]
+    for k, (f, s) in enumerate(g["pairs128"]):
+        got = np.asarray(cube[t0:t1, f, s, 0:2], np.float64)
+        np.testing.assert_allclose(got, g["kl128"][k], rtol=0, atol=1e-6)
+        # planes 2 / 3 repeat 0 / 1 for phase screens
+        np.testing.assert_array_equal(np.asarray(cube[t0:t1, f, s, 2:4]),
+                                      np.asarray(cube[t0:t1, f, s, 0:2]))
+    ph = np.asarray(g["val"])
+    corr = ph - ph[:, :, 0:1, :]
+    px, py = sin_world2pix(g["radec_patch"][:, 0], g["radec_patch"][:, 1],
+                           (126.23, 64.5), (64.0, 64.0), (-0.02602, 0.02602))
+    np.testing.assert_allclose(np.stack([px, py]), g["patch_pix128"], atol=1e-9)
+    n_in = 0
+    for i in range(len(px)):
+        col, row = int(np.round(px[i])), int(np.round(py[i]))
+        if 0 <= row < 128 and 0 <= col < 128:
+            n_in += 1
+            for p, fn in ((0, np.cos), (1, np.sin), (2, np.cos), (3, np.sin)):
+                err = np.abs(np.asarray(cube[:, :, :, p, row, col]) - fn(corr[..., i]))
+                assert np.all(err < 1e-1), (i, p, err.max())
+    assert n_in >= 5
+    del cube
+
+
+def test_kl_evaluators_own_their_context(ctx, dev):
+    """Two KL evaluators of different bases on same-shaped grids, used
+    alternately, and the process-wide context re-based in between (what a
+    refit does): each keeps evaluating its own basis."""
+    from ska_sdp_screen_fitting_amd import geometry
+    from ska_sdp_screen_fitting_amd.kl_screen import KLEvaluator
+    from ska_sdp_screen_fitting_amd.synthetic import make_solutions
+    evs, wants = [], []
+    rng = np.random.default_rng(11)
+    coef = rng.normal(0, 0.01, size=(9, 12))
+    for seed in (1, 2):
+        s = make_solutions(n_ant=2, n_time=1, n_freq=1, n_dir=12, seed=seed)
+        pp, mra, mdec = geometry.piercepoints(s.dir_radec)
+        x, y = geometry.grid_coords(FIELD["rad"], FIELD["dec"], FIELD["width"],
+                                    0.2, mra, mdec)
+        evs.append(KLEvaluator(pp, 100.0, 5.0 / 3.0, x, y, 0))
+        cpix = okl.cpix_matrix(pp, x, y)
+        wants.append(okl.eval_planes(okl.eval_phase_screens(coef, cpix)))
+    for rep in range(2):
+        for ev, want in zip(evs, wants):
+            got = ev.eval_host(coef)
+            np.testing.assert_allclose(got.reshape(want.shape), want, rtol=0, atol=2e-6)
+        # the fit re-bases the shared context (and clears its grid)
+        ctx.set_basis(np.stack([np.linspace(-900, 900, 5), np.zeros(5), np.zeros(5)], 1))
+
+
+def test_kl_write_smoothing(ctx, dev):
+    """KLScreen.write with smooth_pix > 0 (screen.py:353-378): evaluate, then
+    the Gaussian, then the NaN scrub -- vs the oracle planes through scipy."""
+    from oracle import voronoi as ov
+    from ska_sdp_screen_fitting_amd import geometry
+    from ska_sdp_screen_fitting_amd._lib import SF_EVAL_FAST_SINCOS, SF_EVAL_NAN_SCRUB
+    from ska_sdp_screen_fitting_amd.kl_screen import KLEvaluator
+    from ska_sdp_screen_fitting_amd.synthetic import make_solutions
+    s = make_solutions(n_ant=2, n_time=1, n_freq=1, n_dir=9, seed=8)
+    pp, mra, mdec = geometry.piercepoints(s.dir_radec)
+    x, y = geometry.grid_coords(FIELD["rad"], FIELD["dec"], FIELD["width"],
+                                0.05, mra, mdec)
+    ev = KLEvaluator(pp, 100.0, 5.0 / 3.0, x, y, 0)
+    rng = np.random.default_rng(3)
+    coef = rng.normal(0, 0.01, size=(6, 9))
+    coef[2, 4] = np.nan
+    c = torch.from_numpy(coef).to(dev)
+    out = ev.eval_device(c, flags=SF_EVAL_FAST_SINCOS)
+    ev.smooth_device(out, 2.5, SF_EVAL_NAN_SCRUB)
+    torch.cuda.synchronize()
+    planes = okl.eval_planes(okl.eval_phase_screens(coef, okl.cpix_matrix(pp, x, y)))
+    want = ov.smooth(planes.reshape(6, 4, len(y), len(x)).astype(np.float32), 2.5)
+    for p in range(4):
+        v = want[:, p]
+        v[np.isnan(v)] = 0.0 if p % 2 else 1.0
+    np.testing.assert_allclose(out.cpu().numpy(), want, rtol=0, atol=2e-6)
+    assert np.all(out[2, 0].cpu().numpy() == 1.0)
+
+
 def test_make_aterm_image_from_h5parm_file(tmp_path):
     """The same drop-in call on a DP3-layout .h5 (built-in HDF5 reader) gives
     the same FITS cube as the .npz input."""

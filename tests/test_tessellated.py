@@ -94,8 +94,10 @@ def _tess_gpu(lab, phase, smooth):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cell,smooth", [(0.2, 0.0), (0.2, 0.5), (0.05, 1.3),
-                                         (0.02602, 4.0)])
+                                         (0.02602, 4.0), (0.02602, 10.0)])
 def test_tess_kernel_vs_oracle(cell, smooth):
+    """Fused gather + Gaussian (smooth <= 6 px) and, at 10 px (radius 40),
+    gather then the separable passes of sf_smooth -- both vs scipy."""
     g, radec = fixture_patches()
     lab, _ = tessellation_template(radec, FIELD["rad"], FIELD["dec"],
                                    FIELD["width"], cell)
@@ -149,3 +151,56 @@ def test_make_aterm_image_fixture_tessellated(tmp_path):
                                    FIELD["width"], 0.2)
     want = ov.smooth(ov.gather_planes(lab, corr), 0.5)
     np.testing.assert_allclose(cube, want, rtol=0, atol=1e-6)
+
+
+def _scrub(planes):
+    out = planes.copy()
+    for p in range(4):
+        v = out[..., p, :, :]
+        v[np.isnan(v)] = 0.0 if p % 2 else 1.0
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sigma", [0.7, 10.0, 23.5])
+def test_smooth_vs_scipy(sigma):
+    """sf_smooth (any radius) vs scipy.ndimage.gaussian_filter per image,
+    a non-square grid smaller than the radius, one NaN pixel spreading over
+    its neighbourhood, then the scrub (screen.py:353-378 order) and the FITS
+    byte swap."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from ska_sdp_screen_fitting_amd import get_context
+    from ska_sdp_screen_fitting_amd._lib import SF_EVAL_BIG_ENDIAN, SF_EVAL_NAN_SCRUB
+    dev = torch.device("cuda", 0)
+    ctx = get_context(0)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    rng = np.random.default_rng(int(sigma * 10))
+    S, ny, nx = 3, 37, 53
+    cube = rng.normal(size=(S, 4, ny, nx)).astype(np.float32)
+    cube[1, 2, 5, 7] = np.nan
+    want = _scrub(ov.smooth(cube, sigma))
+    for flags in (SF_EVAL_NAN_SCRUB, SF_EVAL_NAN_SCRUB | SF_EVAL_BIG_ENDIAN):
+        d = torch.from_numpy(cube.copy()).to(dev)
+        ctx.smooth(d, nx, ny, 4 * S, sigma, flags)
+        torch.cuda.synchronize()
+        got = d.cpu().numpy()
+        if flags & SF_EVAL_BIG_ENDIAN:
+            got = got.byteswap()
+        np.testing.assert_allclose(got, want, rtol=0, atol=1e-6)
+    assert np.isnan(ov.smooth(cube, sigma)[1, 2]).sum() > 1  # it did spread
+
+
+@pytest.mark.gpu
+def test_tess_rejects_bad_labels():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    lab = np.ones((8, 8), np.int32)
+    lab[3, 3] = 0
+    with pytest.raises(ValueError):
+        _tess_gpu(lab, np.zeros((2, 3)), 0.0)
+    lab[3, 3] = 4
+    with pytest.raises(ValueError):
+        _tess_gpu(lab, np.zeros((2, 3)), 0.0)
