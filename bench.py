@@ -88,9 +88,18 @@ def parse():
     ap.add_argument("--eval-xcd-map", type=int, default=-1,
                     help="SF_OPT_EVAL_XCD_MAP: -1 auto (default), 0 contiguous "
                          "pixel blocks per XCD, 1 interleaved")
+    ap.add_argument("--eval-groups", type=int, default=0,
+                    help="SF_OPT_EVAL_GROUPS: most 16-slot groups per eval work "
+                         "item (0 = library default)")
     ap.add_argument("--checksum", default="auto", choices=("auto", "on", "off"),
                     help="per-slot output checksums (sf_kl_eval_sums); auto: on "
                          "for config4 / config5, whose cubes are discarded")
+    ap.add_argument("--screen", default="phase", choices=("phase", "gain"),
+                    help="gain: phase + slow XX / YY amplitude screens "
+                         "(kl_screen.py:96-125, 319-378): per step the phase "
+                         "fit and the two log10-amplitude fits (niter 3, "
+                         "block sigma over all times, so one time chunk), "
+                         "then the three-contraction gain evaluation")
     ap.add_argument("--eval-only", action="store_true",
                     help="time only sf_kl_eval (profiling)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
@@ -210,7 +219,7 @@ def fits_wallclock():
 
 
 def sampled_slots_check(ctx, torch, dev, setup, coef, N, flags, slot_sums,
-                        n_evals, fast):
+                        n_evals, fast, cxx=None, cyy=None):
     """Parity of sampled slots of the timed run (not timed): slots 0, S/2 and
     S-1 evaluated alone vs an fp64 torch restatement of kl_screen.py:444-449
     (|d| <= 2e-6 with the fp32 sincos epilogue, 1e-6 with fp64), and -- in
@@ -229,15 +238,25 @@ def sampled_slots_check(ctx, torch, dev, setup, coef, N, flags, slot_sums,
     S = coef.shape[0]
     err, sums_ok, slots = 0.0, True, sorted({0, S // 2, S - 1})
     for k in slots:
-        ctx.eval(coef[k:k + 1], 1, one, 1, flags)
+        if cxx is None:
+            ctx.eval(coef[k:k + 1], 1, one, 1, flags)
+        else:
+            ctx.eval_gain(coef[k:k + 1], cxx[k:k + 1], cyy[k:k + 1], 1, one, 1, flags)
         torch.cuda.synchronize(dev)
         ph = cpix @ coef[k]
         c, s = torch.cos(ph), torch.sin(ph)
-        want = torch.stack([c, s, c, s])
+        if cxx is None:
+            want = torch.stack([c, s, c, s])
+            scale = torch.ones_like(want)
+        else:  # kl_screen.py:338-378: 10 ** screen x cos / sin
+            ax, ay = 10.0 ** (cpix @ cxx[k]), 10.0 ** (cpix @ cyy[k])
+            want = torch.stack([ax * c, ax * s, ay * c, ay * s])
+            # gain tolerance relative to max(1, amplitude) (tests/test_gain.py)
+            scale = torch.clamp(torch.stack([ax, ax, ay, ay]), min=1.0)
         got = one[0].reshape(4, P).double()
         live = ~torch.isnan(ph)  # NaN pixels are scrubbed to 1 / 0
         if bool(live.any()):
-            err = max(err, float((got - want)[:, live].abs().max()))
+            err = max(err, float(((got - want) / scale)[:, live].abs().max()))
         if slot_sums is not None:
             h = int((one.view(torch.int32).to(torch.int64) & 0xFFFFFFFF).sum())
             sums_ok &= (h * n_evals) % 2 ** 32 == int(slot_sums[k]) % 2 ** 32
@@ -268,15 +287,15 @@ def _profile_entry(name, workload, kernel):
     return None
 
 
-def mfma_line(kernel, launch_slots, P, D, launch_s, workload):
+def mfma_line(kernel, launch_slots, P, D, launch_s, workload, n_contract=1):
     """fp64 MFMA work of one evaluation launch: executed flops (the k-steps
     padded to a multiple of 4 directions) and the algorithmic 2 D flops per
     pixel per slot, over the launch time, against the fp64 matrix peak; the
     MFMA-busy fraction from PMC counters when profiles/mfma.json holds this
     workload."""
     ks = (D + 3) // 4
-    executed = launch_slots * P * 2.0 * 4 * ks
-    algo = launch_slots * P * 2.0 * D
+    executed = launch_slots * P * 2.0 * 4 * ks * n_contract
+    algo = launch_slots * P * 2.0 * D * n_contract
     res = {"kernel": kernel, "unit": "TFLOP/s", "peak": FP64_MFMA_PEAK_TFS,
            "executed": executed / launch_s / 1e12,
            "algorithmic": algo / launch_s / 1e12,
@@ -289,8 +308,8 @@ def mfma_line(kernel, launch_slots, P, D, launch_s, workload):
     return res
 
 
-def side_legs(ctx, torch, dev, stream, fit_stream, fit, coef, bounds, F, A,
-              D, P, out, ring, flags):
+def side_legs(ctx, torch, dev, stream, fit_stream, fit, evaluate, coef, bounds,
+              F, A, D, P, out, ring, flags, gain=False, amp=None):
     """Untimed side measurements after the timed steps: (1) the evaluation of
     time chunk 0 with the fp64 sincos epilogue (--precise-sincos) beside the
     default fp32 one, (2) the fit of chunk 0 alone on the whole chip.  HIP
@@ -314,12 +333,19 @@ def side_legs(ctx, torch, dev, stream, fit_stream, fit, coef, bounds, F, A,
             ms.append(e0.elapsed_time(e1))
         return float(np.mean(ms))
 
+    def ev(fl):
+        if gain:
+            ctx.eval_gain(c0, amp["coef"][0][t0:t1].reshape(-1, D),
+                          amp["coef"][1][t0:t1].reshape(-1, D), n, out, ring, fl)
+        else:
+            ctx.eval(c0, n, out, ring, fl)
+
     for name, fl in (("eval_fp32_sincos", flags),
                      ("eval_fp64_sincos", flags & ~SF_EVAL_FAST_SINCOS)):
         ctx.set_stream(stream.cuda_stream)
-        ms = timed(lambda: ctx.eval(c0, n, out, ring, fl), stream)
-        gbs = n * (16 * P + 8 * D) / ms / 1e6
-        res[name] = {"kernel": ctx.eval_kernel(fl), "slots": n,
+        ms = timed(lambda: ev(fl), stream)
+        gbs = n * (16 * P + 8 * D * (3 if gain else 1)) / ms / 1e6
+        res[name] = {"kernel": ctx.eval_kernel(fl, gain=gain), "slots": n,
                      "launch_ms": ms, "slots_per_s": n / ms * 1e3,
                      "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS}
     ms = timed(lambda: fit(0, fit_stream), fit_stream)
@@ -354,11 +380,14 @@ def main():
     from ska_sdp_screen_fitting_amd._lib import (SF_EVAL_FAST_SINCOS,
                                                  SF_EVAL_NAN_SCRUB,
                                                  SF_EVAL_NT_STORES,
+                                                 SF_OPT_EVAL_GROUPS,
                                                  SF_OPT_EVAL_XCD_MAP)
     from ska_sdp_screen_fitting_amd.distributed import setup_shard
+    from ska_sdp_screen_fitting_amd._lib import SF_SCREEN_AMPLITUDE
     from ska_sdp_screen_fitting_amd.synthetic import (FIELD_DEC_DEG,
                                                       FIELD_RA_DEG,
                                                       FIELD_WIDTH_DEG,
+                                                      make_amplitudes,
                                                       make_solutions)
 
     A, T, F, D, N, cell = WORKLOADS[args.workload]
@@ -397,6 +426,28 @@ def main():
     out = torch.empty((ring, 4, N, N), dtype=torch.float32, device=dev)
     flags = (SF_EVAL_NAN_SCRUB | SF_EVAL_NT_STORES
              | (0 if args.precise_sincos else SF_EVAL_FAST_SINCOS))
+    gain = args.screen == "gain"
+    amp = None
+    if gain:
+        # slow XX / YY amplitudes on the phase grid; fitted in log10 space
+        # with order min(12, max(3, round(D / 2))), no order scaling, no
+        # reference station, 3 iterations (kl_screen.py:96-125)
+        make_amplitudes(sol)
+        order_amp = min(12, max(3, int(np.round(D / 2))))
+        amp = {"order": order_amp, "val": [], "w": [], "coef": [], "resid": [],
+               "w_out": [], "orders": []}
+        for p in range(2):
+            v = torch.from_numpy(np.ascontiguousarray(sol.amp_val[..., p])).to(dev)
+            w = torch.from_numpy(np.ascontiguousarray(sol.meta["amp_weight"][..., p])).to(dev)
+            amp["val"].append(v)
+            amp["w"].append(w)
+            amp["coef"].append(torch.empty_like(v))
+            amp["resid"].append(torch.empty_like(v))
+            amp["w_out"].append(torch.empty_like(w))
+            amp["orders"].append(torch.empty((T, F, A), dtype=torch.int32, device=dev))
+        # the amplitude outlier sigma couples every time of a (freq,
+        # station) block (Q6): the fit sees all times at once
+        args.chunks = 1
 
     # time chunks (the solution layout is time-major, so a chunk is a
     # contiguous slice of every array); phase slots are independent, so the
@@ -434,7 +485,8 @@ def main():
                 fit_stream = torch.cuda.ExternalStream(fit_handle, device=dev)
 
     ctx.set_option(SF_OPT_EVAL_XCD_MAP, args.eval_xcd_map)
-    eval_kernel_name = ctx.eval_kernel(flags)
+    ctx.set_option(SF_OPT_EVAL_GROUPS, args.eval_groups)
+    eval_kernel_name = ctx.eval_kernel(flags, gain=gain)
     # discard + checksum mode: the cubes go
     # through the HBM ring and every slot's checksum is accumulated
     checksum = args.checksum == "on" or (args.checksum == "auto"
@@ -449,14 +501,29 @@ def main():
                 coef=coef[t0:t1], resid=resid[t0:t1], w_out=w_out[t0:t1],
                 order_out=order_out[t0:t1], ant_offset=setup["ant_offset"],
                 ref_phase=refph[t0:t1])
+        if gain:
+            for p in range(2):
+                ctx.fit(amp["val"][p][t0:t1], amp["w"][p][t0:t1], t1 - t0, F, A,
+                        [amp["order"]] * A, screen_type=SF_SCREEN_AMPLITUDE,
+                        niter=3, nsigma=5.0, adjust_order=True, ref_ant=-1,
+                        coef=amp["coef"][p][t0:t1], resid=amp["resid"][p][t0:t1],
+                        w_out=amp["w_out"][p][t0:t1],
+                        order_out=amp["orders"][p][t0:t1])
 
     def evaluate(c):
         t0, t1 = bounds[c]
         ctx.set_stream(stream.cuda_stream)
         n = (t1 - t0) * F * A
+        cxx = cyy = None
+        if gain:
+            cxx = amp["coef"][0][t0:t1].reshape(-1, D)
+            cyy = amp["coef"][1][t0:t1].reshape(-1, D)
         if checksum:
             ctx.eval_sums(coef[t0:t1].reshape(-1, D), n, out,
-                          slot_sums[t0 * F * A:t1 * F * A], ring, flags=flags)
+                          slot_sums[t0 * F * A:t1 * F * A], ring, coef_xx=cxx,
+                          coef_yy=cyy, flags=flags)
+        elif gain:
+            ctx.eval_gain(coef[t0:t1].reshape(-1, D), cxx, cyy, n, out, ring, flags)
         else:
             ctx.eval(coef[t0:t1].reshape(-1, D), n, out, ring, flags)
 
@@ -532,21 +599,25 @@ def main():
     # parity spot check (cheap invariants, not timed): cos^2 + sin^2 = 1
     chk = out[: min(ring, 64)].float()
     unit_err = float((chk[:, 0] ** 2 + chk[:, 1] ** 2 - 1).abs().max())
-    sampled = sampled_slots_check(ctx, torch, dev, setup, coef.reshape(-1, D), N,
-                                  flags, slot_sums, args.warmup + args.steps,
-                                  not args.precise_sincos)
+    sampled = sampled_slots_check(
+        ctx, torch, dev, setup, coef.reshape(-1, D), N, flags, slot_sums,
+        args.warmup + args.steps, not args.precise_sincos,
+        cxx=amp["coef"][0].reshape(-1, D) if gain else None,
+        cyy=amp["coef"][1].reshape(-1, D) if gain else None)
 
     side = {}
     if not args.no_side_legs and not args.eval_only:
-        side = side_legs(ctx, torch, dev, stream, first_fit_stream, fit, coef,
-                         bounds, F, A, D, P, out, ring, flags)
+        side = side_legs(ctx, torch, dev, stream, first_fit_stream, fit, evaluate,
+                         coef, bounds, F, A, D, P, out, ring, flags, gain, amp)
 
     if rank == 0:
-        algo_bytes = S * (16 * P + 8 * D)  # SURVEY.md §8(d), per step
+        # SURVEY.md §8(d), per step; gain screens read three coefficient sets
+        algo_bytes = S * (16 * P + 8 * D * (3 if gain else 1))
         launch_bytes = algo_bytes / n_chunks  # per eval launch (equal chunks)
         achieved = launch_bytes / t_eval_launch / 1e9
         traffic = None
-        tj = _profile_entry("traffic.json", args.workload, eval_kernel_name)
+        wkey = args.workload + ("-gain" if gain else "")
+        tj = _profile_entry("traffic.json", wkey, eval_kernel_name)
         if (tj is not None and tj.get("flags") == flags
                 and tj.get("chunks", 1) == n_chunks):
             traffic = tj.get("hbm_bytes_per_launch")
@@ -564,10 +635,16 @@ def main():
             "dtype": "f64",
             "data": "synthetic",
             "config": {
-                "workload": (f"{args.workload}: {A_total} ant x {T} time x {F} freq x "
+                "workload": (f"{args.workload}{'-gain' if gain else ''}: {A_total} ant x "
+                             f"{T} time x {F} freq x "
                              f"{D} dir, {A} ant per GPU (ant-sharded, "
                              f"{'strong' if strong else 'weak'} scaling), KL {N}^2 "
-                             "screen, fit (phase, niter 2, adjust_order) + eval"),
+                             + ("gain screens: phase fit (niter 2) + XX / YY "
+                                "log10-amplitude fits (niter 3, order "
+                                f"{amp['order']}) + 3-contraction eval with 10**"
+                                if gain else
+                                "screen, fit (phase, niter 2, adjust_order) + eval")),
+                "screen": args.screen,
                 "slots_per_gpu": S, "grid": N, "n_dir": D,
                 "parallelism": f"ant-shard x{world}",
                 "eval_sincos": "fp64" if args.precise_sincos else "fp32-after-fp64-reduction",
@@ -585,7 +662,7 @@ def main():
                 "launch_ms": t_eval_launch * 1e3,
             },
             "mfma": mfma_line(eval_kernel_name, S / n_chunks, P, D,
-                              t_eval_launch, args.workload),
+                              t_eval_launch, wkey, 3 if gain else 1),
             "stages_ms": {"fit": t_fit * 1e3, "eval": t_eval * 1e3,
                           "overlap": "fit(c+1) || eval(c), %d time chunks" % n_chunks
                           if n_chunks > 1 else "none"},

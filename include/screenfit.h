@@ -128,9 +128,10 @@ int sf_device_cus(sf_ctx* ctx, int* n_cu);
  * blocks pb = x (mod 8); -1 (default): 1 when an XCD's eighth is at most 8
  * pixel blocks (256^2 with 4 KiB runs: +2-3 % measured), else 0. */
 #define SF_OPT_EVAL_XCD_MAP 7
-/* SF_OPT_EVAL_GROUPS = g (1..256, power of two; 0 = auto = 256): most
- * 16-slot groups per evaluation work item (each item loads its pixel block's
- * basis once, so longer items re-read less of it). */
+/* SF_OPT_EVAL_GROUPS = g (1..256, power of two; 0 = auto: 64 for the
+ * register-tile kernels, 16 for the LDS-staged ones): most 16-slot groups per
+ * evaluation work item (each item loads its pixel block's basis once, so
+ * longer items re-read less of it). */
 #define SF_OPT_EVAL_GROUPS 8
 #define SF_EVAL_KERNEL_AUTO 0
 #define SF_EVAL_KERNEL_TILE 1

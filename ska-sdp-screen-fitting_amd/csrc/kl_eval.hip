@@ -200,11 +200,12 @@ __device__ __forceinline__ void store4(float* p, v4f v) {
   else *reinterpret_cast<v4f*>(p) = v;
 }
 
-template <bool FAST>
-__device__ __forceinline__ double amp10(double x) {
-  // amplitude screens are log10 values: 10 ** screen (kl_screen.py:338-365)
-  if (FAST) return (double)exp10f((float)x);
-  return exp10(x);
+// amplitude screens are log10 values: 10 ** screen (kl_screen.py:338-365);
+// fast path: the XX / YY coefficients are pre-scaled by log2(10), so the
+// contraction gives log2 A, rounded to float for v_exp_f32 (1 ulp)
+constexpr double kLog2of10 = 3.321928094887362;
+__device__ __forceinline__ float amp2f(double log2a) {
+  return __builtin_amdgcn_exp2f((float)log2a);
 }
 
 // SHB ("shared B"): the 4 waves of a workgroup share ONE 64-pixel block,
@@ -266,6 +267,12 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
       if constexpr (SHB) asm volatile("" ::: "memory");
       double af[KS];
       load_coef<KS>(af, coef, s0, S, D, l, FAST ? kInv2Pi : 1.0);
+      // gain: the XX / YY coefficient loads go out with the phase ones
+      double ax[GAIN ? KS : 1], ay[GAIN ? KS : 1];
+      if constexpr (GAIN) {
+        load_coef<KS>(ax, coef_xx, s0, S, D, l, FAST ? kLog2of10 : 1.0);
+        load_coef<KS>(ay, coef_yy, s0, S, D, l, FAST ? kLog2of10 : 1.0);
+      }
       // ring slot of the group's first slot (S, ring < 2^31: launch_eval);
       // the 16 rows follow it with at most one wrap when the ring is >= 16
       // slots -- scalar, no per-lane 64-bit modulo
@@ -281,10 +288,7 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
                                                         acc[t], 0, 0, 0);
       // gain: the XX / YY log-amplitude screens share the pixel basis
       v4d accx[GAIN ? kTiles : 1], accy[GAIN ? kTiles : 1];
-      if (GAIN) {
-        double ax[KS], ay[KS];
-        load_coef<KS>(ax, coef_xx, s0, S, D, l, 1.0);
-        load_coef<KS>(ay, coef_yy, s0, S, D, l, 1.0);
+      if constexpr (GAIN) {
 #pragma unroll
         for (int t = 0; t < kTiles; ++t) {
           accx[t] = v4d{0.0, 0.0, 0.0, 0.0};
@@ -320,13 +324,23 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
             // a NaN phase stays NaN through A * cos and is scrubbed below,
             // as the reference scrubs the product (screen.py:368-378)
             jones_sincos<FAST>(acc[t][r], sf, cf, false);
-            // reference: A (fp64) * cos (fp64), one cast at the FITS store
-            const double ax = amp10<FAST>(accx[t][r]);
-            const double ay = amp10<FAST>(accy[t][r]);
-            pv[0][t] = (float)(ax * (double)cf);
-            pv[1][t] = (float)(ax * (double)sf);
-            pv[2][t] = (float)(ay * (double)cf);
-            pv[3][t] = (float)(ay * (double)sf);
+            if (FAST) {
+              // fp32 amplitude x fp32 cos / sin: within 2e-6 x max(1, A)
+              const float ax = amp2f(accx[t][r]);
+              const float ay = amp2f(accy[t][r]);
+              pv[0][t] = ax * cf;
+              pv[1][t] = ax * sf;
+              pv[2][t] = ay * cf;
+              pv[3][t] = ay * sf;
+            } else {
+              // reference: A (fp64) * cos (fp64), one cast at the FITS store
+              const double ax = exp10(accx[t][r]);
+              const double ay = exp10(accy[t][r]);
+              pv[0][t] = (float)(ax * (double)cf);
+              pv[1][t] = (float)(ax * (double)sf);
+              pv[2][t] = (float)(ay * (double)cf);
+              pv[3][t] = (float)(ay * (double)sf);
+            }
           } else {
             // FAST: NaN scrubbed on the reduced argument (cos 1, sin 0)
             jones_sincos<FAST>(acc[t][r], sf, cf, scrub);
@@ -557,12 +571,15 @@ static int64_t eval_grid(const sf_ctx* ctx, int64_t n_pb, int64_t n_sc,
 }
 
 // 16-slot groups per (pixel block, slot chunk) work item: as many as keep
-// >= min_items items (the grid fills the chip), at most max_groups.  Every
-// item loads its pixel block's Cpix fragments once, so long chunks keep that
-// reload small against the item's output: at 512^2 x D = 50 the Cpix of one
-// XCD's pixel blocks (13.6 MB) outgrows its 4 MiB L2, and 16 groups per item
-// re-read 3.6 TB of it per 8.2 M-slot launch (FETCH_SIZE, 10 % of the
-// writes); 256 groups (4096 slots) cut that 16x.
+// >= min_items items (the grid fills the chip), at most max_groups
+// (SF_OPT_EVAL_GROUPS, else 64 for the register tile, 16 for the LDS-staged
+// kernels).  Every item loads its pixel block's Cpix fragments once, so long
+// chunks keep that reload small against the item's output: at 512^2 x D = 50
+// the Cpix of one XCD's pixel blocks (13.6 MB) outgrows its 4 MiB L2, and 16
+// groups per item re-read 3.6 TB of it per 8.2 M-slot launch (FETCH_SIZE,
+// 10 % of the writes; 64 groups: 0.9 TB, +2 %); at 256^2 x D = 20 the slices
+// stay in L2 and 16 groups keep each XCD's coefficient rows there too
+// (profiles/round2e_eval_groups_ab.txt, round2f_eval_groups_bench.txt).
 static int eval_chunk_groups(int64_t n_pb, int64_t S, int max_groups,
                              int64_t min_items) {
   int groups = max_groups;
@@ -589,7 +606,7 @@ static int launch_eval_ks(sf_ctx* ctx, const double* coef,
                           unsigned* sums) {
   const int64_t P = ctx->n_pix;
   const int64_t n_pb = ctx->n_pix_blocks;
-  const int groups = eval_chunk_groups(n_pb, S, ctx->eval_groups ? ctx->eval_groups : 256, 2048);
+  const int groups = eval_chunk_groups(n_pb, S, ctx->eval_groups ? ctx->eval_groups : 64, 2048);
   const int64_t n_sc = (S + 16 * groups - 1) / (16 * groups);
   const int64_t nblk = eval_grid(ctx, n_pb, n_sc, 256);
   const bool vec4 = (P % 4 == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
@@ -630,7 +647,7 @@ static int launch_eval_shb(sf_ctx* ctx, const double* coef, int64_t S,
                            unsigned* sums) {
   const int64_t P = ctx->n_pix;
   const int64_t n_wpb = ctx->n_pix_blocks * kEvalWaves;
-  const int groups = eval_chunk_groups(n_wpb, S, ctx->eval_groups ? ctx->eval_groups : 256, 4096);
+  const int groups = eval_chunk_groups(n_wpb, S, ctx->eval_groups ? ctx->eval_groups : 64, 4096);
   const int64_t n_sc = (S + 16 * groups - 1) / (16 * groups);
   const int64_t nblk = eval_grid(ctx, n_wpb, n_sc, 256);
   const bool fast = flags & SF_EVAL_FAST_SINCOS;
@@ -657,7 +674,7 @@ static int launch_eval_lds(sf_ctx* ctx, const double* coef, int64_t S,
   const int64_t P = ctx->n_pix;
   const int64_t run = EvalLds<NW, TPW>::kRun;
   const int64_t n_pb = (P + run - 1) / run;
-  const int groups = eval_chunk_groups(n_pb, S, ctx->eval_groups ? ctx->eval_groups : 256, 1024);
+  const int groups = eval_chunk_groups(n_pb, S, ctx->eval_groups ? ctx->eval_groups : 16, 1024);
   const int64_t n_sc = (S + 16 * groups - 1) / (16 * groups);
   const int64_t nblk = eval_grid(ctx, n_pb, n_sc, 64 * NW);
   // auto XCD map: interleave the pixel blocks over the XCDs when each XCD's

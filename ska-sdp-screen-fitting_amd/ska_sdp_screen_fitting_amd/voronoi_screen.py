@@ -78,6 +78,15 @@ def rasterize_cell(ring, n):
 def tessellation_template(patch_radec, rad, dec, width_deg, cellsize_deg):
     """voronoi_screen.py:218-351 -> (labels [ny, nx] int32 in 1..D, patch xy).
     Cells are painted in direction order (later cells win a shared pixel)."""
+    rings, xy, n = _rings(patch_radec, rad, dec, width_deg, cellsize_deg)
+    return paint_cells(rings, n), xy
+
+
+def _rings(patch_radec, rad, dec, width_deg, cellsize_deg):
+    """Voronoi cell rings in pixel coordinates (voronoi_screen.py:230-309):
+    SIN pixel positions of the patches, the field box, a 64-point outer ring
+    closing the tessellation; each direction's bounded region, its vertices
+    in counter-clockwise angle order about their mean."""
     n = geometry.grid_size(width_deg, cellsize_deg)
     crval, crpix, cdelt = (rad, dec), (n / 2.0, n / 2.0), (-cellsize_deg, cellsize_deg)
     ra = np.asarray(patch_radec, np.float64)[:, 0]
@@ -108,6 +117,18 @@ def tessellation_template(patch_radec, rad, dec, width_deg, cellsize_deg):
             v = v[np.argsort(np.arctan2(v[:, 1] - ctr[1], v[:, 0] - ctr[0]))]
             pts = [(float(a), float(b)) for a, b in v]
             rings.append(pts + [pts[0]])
+    return rings, xy, n
+
+
+def paint_cells(rings, n):
+    """voronoi_screen.py:319-349: rasterize every cell ring (label = index +
+    1) in list order -- a pixel claimed by two cells (its centre exactly on
+    their shared edge: the exact border test keeps it in both) takes the
+    later one -- then give uncovered pixels the nearest painted label
+    (griddata 'nearest' in index space).  The reference paints in shapely
+    polygonize order (GEOS's edge-ring order, not reproducible here); on the
+    fixture no pixel is claimed twice at 0.2, 0.1, 0.05 or 0.02602 deg
+    (tests/test_tessellated.py), so the order does not matter there."""
     labels = np.zeros((n, n), np.int32)
     for i, ring in enumerate(rings):
         labels[rasterize_cell(ring, n)] = i + 1
@@ -117,7 +138,12 @@ def tessellation_template(patch_radec, rad, dec, width_deg, cellsize_deg):
         zy, zx = np.nonzero(empty)
         labels[empty] = si.griddata((iy, ix), labels[~empty], (zy, zx),
                                     method="nearest")
-    return labels, xy
+    return labels
+
+
+def cell_rings(patch_radec, rad, dec, width_deg, cellsize_deg):
+    """The closed pixel-space rings of tessellation_template (for tests)."""
+    return _rings(patch_radec, rad, dec, width_deg, cellsize_deg)[0]
 
 
 def gaussian_weights(smooth_pix, truncate=4.0):

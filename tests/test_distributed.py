@@ -26,6 +26,26 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def _slot_checksums(phi, w, st_order, pp, x, y, slots, ref_local=None):
+    """Oracle fit + evaluation of sampled (t, f, a) slots of a [T, F, A, D]
+    referenced block -> the sf_kl_eval_sums checksum of each slot's float32
+    cube (sum mod 2^32 of its 32-bit words)."""
+    from oracle import kl as okl
+    basis = okl.Basis(pp)
+    cpix = okl.cpix_matrix(pp, x, y)
+    out = []
+    for t, f, a in slots:
+        if a == ref_local:  # the reference station keeps zero coefficients
+            white = np.zeros(phi.shape[-1])
+        else:
+            white = okl.fit_slot(phi[t, f, a], w[t, f, a], st_order[a],
+                                 st_order[a], basis)[0]
+        planes = okl.eval_planes(okl.eval_phase_screens(white[None, :], cpix))
+        words = planes.astype(np.float32).view(np.uint32).astype(np.uint64)
+        out.append(int(words.sum() % 2 ** 32))
+    return out
+
+
 def _worker(rank, world, port, outdir):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -35,9 +55,18 @@ def _worker(rank, world, port, outdir):
                            ant_offset=a0, n_ant_total=N_TOTAL, flag_frac=0.05)
     st = setup_shard(local, a0, N_TOTAL, FIELD_RA_DEG, FIELD_DEC_DEG,
                      FIELD_WIDTH_DEG, CELL)
+    # this shard's sampled slots, fitted and evaluated from the shard's own
+    # setup (referenced with the broadcast reference phases)
+    phi = local.val - st["ref_phase"].numpy()[:, :, None, :]
+    slots = [(t, 0, a) for t in (0, T - 1) for a in (0, a1 - a0 - 1)]
+    ref = st["ref_ant"]
+    sums = _slot_checksums(phi, local.weight, st["st_order"], st["piercepoints"],
+                           st["x"], st["y"], slots,
+                           ref - a0 if a0 <= ref < a1 else None)
     np.savez(os.path.join(outdir, f"r{rank}.npz"), ref=st["ref_ant"],
              st_order=np.array(st["st_order"]), pp=st["piercepoints"],
-             x=st["x"], y=st["y"], refph=st["ref_phase"].numpy(), a0=a0, a1=a1)
+             x=st["x"], y=st["y"], refph=st["ref_phase"].numpy(), a0=a0, a1=a1,
+             slots=np.array(slots), sums=np.array(sums, np.uint64))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -79,4 +108,11 @@ def test_setup_shard_world2_matches_unsharded(tmp_path):
         np.testing.assert_array_equal(z["y"], y)
         np.testing.assert_array_equal(z["refph"], full.val[:, :, ref, :])
         got_orders += list(z["st_order"])
+        # the shard's sampled slots: the same cube checksums as the same
+        # global slots of the unsharded run
+        a0 = int(z["a0"])
+        phi = full.val - full.val[:, :, ref:ref + 1, :]
+        glob = [(t, f, a0 + a) for t, f, a in z["slots"]]
+        want = _slot_checksums(phi, full.weight, want_orders, pp, x, y, glob, ref)
+        assert [int(v) for v in z["sums"]] == want
     assert got_orders == want_orders

@@ -66,6 +66,72 @@ def test_template_anchors():
     assert int((near != lab).sum()) == 5
 
 
+CONFIG_CELLS = [0.2, 0.1, 0.05, 0.02602]
+
+
+@pytest.mark.parametrize("cell", CONFIG_CELLS)
+def test_patch_pixels_own_their_cell(cell):
+    """The reference test's anchor (tests/test_make_aterm_images.py: the
+    cube at each patch's pixel, via the cube's own SIN WCS, is that patch's
+    value) at every cell size the configs use, down to config 2's 128^2."""
+    from ska_sdp_screen_fitting_amd import geometry
+    g, radec = fixture_patches()
+    lab, xy = tessellation_template(radec, FIELD["rad"], FIELD["dec"],
+                                    FIELD["width"], cell)
+    n = lab.shape[0]
+    assert n == geometry.grid_size(FIELD["width"], cell)
+    assert lab.min() == 1 and lab.max() == len(radec)
+    px, py = geometry.sin_world2pix(g["radec_patch"][:, 0], g["radec_patch"][:, 1],
+                                    (FIELD["rad"], FIELD["dec"]), (n / 2.0, n / 2.0),
+                                    (-cell, cell))
+    n_in = 0
+    for k in range(len(px)):
+        c, r = int(np.round(px[k])), int(np.round(py[k]))
+        if 0 <= r < n and 0 <= c < n:
+            n_in += 1
+            assert lab[r, c] == k + 1, (k, r, c, lab[r, c])
+    assert n_in >= 5
+
+
+@pytest.mark.parametrize("cell", CONFIG_CELLS)
+def test_no_pixel_claimed_twice(cell):
+    """No pixel centre of the fixture's rasters lies on a shared cell edge at
+    the configs' cell sizes, so the painting order -- shapely polygonize
+    order in the reference, direction order here -- cannot change a label."""
+    from ska_sdp_screen_fitting_amd.voronoi_screen import cell_rings, rasterize_cell
+    _, radec = fixture_patches()
+    rings = cell_rings(radec, FIELD["rad"], FIELD["dec"], FIELD["width"], cell)
+    n = tessellation_template(radec, FIELD["rad"], FIELD["dec"], FIELD["width"],
+                              cell)[0].shape[0]
+    claims = sum(rasterize_cell(r, n).astype(int) for r in rings)
+    assert int((claims > 1).sum()) == 0
+
+
+def test_tie_rule_later_cell_wins():
+    """A pixel centre exactly on the edge two cells share is kept by both
+    exact border tests (shapely: on the boundary is not disjoint) and takes
+    the cell painted last."""
+    from ska_sdp_screen_fitting_amd.voronoi_screen import paint_cells, rasterize_cell
+    a = [(0.0, 0.0), (5.0, 0.0), (5.0, 9.0), (0.0, 9.0), (0.0, 0.0)]
+    b = [(5.0, 0.0), (9.0, 0.0), (9.0, 9.0), (5.0, 9.0), (5.0, 0.0)]
+    ma, mb = rasterize_cell(a, 10), rasterize_cell(b, 10)
+    assert ma[:, 5].all() and mb[:, 5].all()  # column x = 5: on both edges
+    lab = paint_cells([a, b], 10)  # b (label 2) painted last
+    assert np.all(lab[:, 5] == 2) and np.all(lab[:, 0] == 1) and np.all(lab[:, 9] == 2)
+    lab = paint_cells([b, a], 10)  # a (label 2) painted last
+    assert np.all(lab[:, 5] == 2) and np.all(lab[:, 0] == 2) and np.all(lab[:, 9] == 1)
+
+
+# Residual, measured: besides the painting order, the reference's labels
+# depend on the start vertex and orientation of each GEOS ring (Pillow draws
+# the outline by lines whose rounding depends on direction, and only outline
+# pixels get the exact test).  Over 40 random (order, start, orientation)
+# conventions the fixture's labels change at <= 2 / 289 (0.2 deg), 1 / 1156
+# (0.1), 16 / 4489 (0.05) and 16 / 16384 pixels (0.02602 deg).  Without
+# shapely / GEOS here the reference's convention cannot be reproduced, so
+# those few pixels stay "parity unpinned" (DESIGN.md).
+
+
 @pytest.mark.parametrize("sigma", [0.5, 1.3, 4.2])
 def test_gaussian_weights_match_scipy(sigma):
     from scipy.ndimage import _filters

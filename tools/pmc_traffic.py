@@ -1,66 +1,102 @@
 #!/usr/bin/env python3
-"""HBM traffic per eval launch from two rocprofv3 PMC passes (separate runs,
-per MI355X_MICROARCH.md): WRITE_SIZE and FETCH_SIZE counter CSVs in KB;
-FETCH_SIZE is doubled (gfx950 correction in the guide).  Writes
-profiles/traffic.json, which bench.py reads when workload / flags / chunks
-match its own run.
+"""Per-launch HBM traffic and MFMA / VALU busy of the evaluation kernel from
+separate rocprofv3 PMC passes (tools/pmc_passes.sh directories), written as
+entries of profiles/traffic.json and profiles/mfma.json (keyed by workload and
+bench.py's roofline.kernel), which bench.py reports as roofline.traffic and
+mfma.busy_frac_pmc when its run matches.
 
-  python tools/pmc_traffic.py WRITE.csv FETCH.csv --workload config3 \
-      --flags 769 --chunks 2 --slots 51200 --grid 256 --n-dir 20 \
+  python tools/pmc_traffic.py --traffic-dir gpurun_out/X/c4eval \
+      --mfma-dir gpurun_out/X/c4 --workload config4 --flags 769 --chunks 2 \
+      --slots 4096000 --grid 256 --n-dir 20 \
       --eval-kernel 'kl_eval_lds_kernel<16 waves>'
+
+WRITE_SIZE / FETCH_SIZE are in KB; FETCH_SIZE is doubled (the gfx950
+correction of MI355X_MICROARCH.md's HBM section).  Counters are averaged over
+the full-grid launches of the evaluation kernel (tools/pmc_summary.py).
 """
 import argparse
-import csv
 import json
 import os
+import subprocess
+import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def per_launch(path, counter, kernel="sf::kl_eval"):
-    vals, name = [], None
-    for r in csv.DictReader(open(path)):
-        if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
-            vals.append(float(r["Counter_Value"]))
-            name = r["Kernel_Name"].split("(")[0]
-    if not vals:
-        raise SystemExit(f"no {kernel} rows with {counter} in {path}")
-    return sum(vals) / len(vals), len(vals), name
+def summary(d, kernel):
+    out = subprocess.run([sys.executable, os.path.join(REPO, "tools", "pmc_summary.py"),
+                          d, "--kernel", kernel], check=True, capture_output=True,
+                         text=True).stdout
+    return json.loads(out)
+
+
+def upsert(path, entry):
+    try:
+        tab = json.load(open(path))
+    except (OSError, ValueError):
+        tab = {}
+    if "entries" not in tab:  # the round-1 single-entry file
+        tab = {"entries": [tab] if tab else []}
+    tab["entries"] = [e for e in tab["entries"]
+                      if not (e.get("workload") == entry["workload"]
+                              and e.get("eval_kernel") == entry["eval_kernel"])]
+    tab["entries"].append(entry)
+    json.dump(tab, open(path, "w"), indent=1)
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("write_csv")
-    ap.add_argument("fetch_csv")
-    ap.add_argument("--workload", default="config3")
+    ap.add_argument("--traffic-dir", help="pmc_passes.sh dir with write/ fetch/")
+    ap.add_argument("--mfma-dir", help="pmc_passes.sh dir with mfma/ occ/")
+    ap.add_argument("--kernel", default="sf::kl_eval")
+    ap.add_argument("--workload", required=True)
     ap.add_argument("--flags", type=int, required=True)
     ap.add_argument("--chunks", type=int, default=1)
     ap.add_argument("--slots", type=int, required=True, help="slots per launch")
     ap.add_argument("--grid", type=int, required=True)
     ap.add_argument("--n-dir", type=int, required=True)
+    ap.add_argument("--coef-sets", type=int, default=1, help="3 for gain screens")
     ap.add_argument("--eval-kernel", required=True,
                     help="bench.py's roofline.kernel for the profiled run")
-    ap.add_argument("--out", default=os.path.join(REPO, "profiles", "traffic.json"))
+    ap.add_argument("--label", default="")
     a = ap.parse_args()
-    w_kb, nw, name = per_launch(a.write_csv, "WRITE_SIZE")
-    f_kb, nf, _ = per_launch(a.fetch_csv, "FETCH_SIZE")
-    wb, fb = w_kb * 1024.0, 2.0 * f_kb * 1024.0
-    algo = a.slots * (16 * a.grid * a.grid + 8 * a.n_dir)
-    out = {
-        "workload": a.workload, "kernel": name, "eval_kernel": a.eval_kernel,
-        "flags": a.flags,
-        "chunks": a.chunks, "launches_averaged": min(nw, nf),
-        "write_bytes": wb, "fetch_bytes_corrected_x2": fb,
-        "hbm_bytes_per_launch": wb + fb,
-        "algorithmic_bytes_per_launch": algo,
-        "ratio_to_algorithmic": (wb + fb) / algo,
-        "sources": [os.path.relpath(a.write_csv, REPO), os.path.relpath(a.fetch_csv, REPO)],
-        "note": "separate rocprofv3 --pmc WRITE_SIZE / FETCH_SIZE passes of "
-                "bench.py --eval-only; KB units; FETCH_SIZE doubled per the "
-                "MI355X_MICROARCH.md HBM section",
-    }
-    json.dump(out, open(a.out, "w"), indent=1)
-    print(json.dumps(out, indent=1))
+    algo = a.slots * (16 * a.grid * a.grid + 8 * a.n_dir * a.coef_sets)
+    if a.traffic_dir:
+        r = summary(a.traffic_dir, a.kernel)
+        d = r["derived"]
+        wb, fb = d["write_bytes"], d["fetch_bytes_x2"]
+        entry = {
+            "workload": a.workload, "kernel": r["kernel"], "eval_kernel": a.eval_kernel,
+            "flags": a.flags, "chunks": a.chunks, "launches_averaged": r["dispatches"],
+            "write_bytes": wb, "fetch_bytes_corrected_x2": fb,
+            "hbm_bytes_per_launch": wb + fb,
+            "algorithmic_bytes_per_launch": algo,
+            "ratio_to_algorithmic": (wb + fb) / algo,
+            "source": os.path.relpath(a.traffic_dir, REPO), "label": a.label,
+            "note": "separate rocprofv3 --pmc WRITE_SIZE / FETCH_SIZE passes of "
+                    "bench.py --eval-only; FETCH_SIZE doubled (MI355X_MICROARCH.md)",
+        }
+        upsert(os.path.join(REPO, "profiles", "traffic.json"), entry)
+        print(json.dumps(entry, indent=1))
+    if a.mfma_dir:
+        r = summary(a.mfma_dir, a.kernel)
+        d = r["derived"]
+        entry = {
+            "workload": a.workload, "kernel": r["kernel"], "eval_kernel": a.eval_kernel,
+            "mfma_busy_frac": d.get("mfma_busy_frac"),
+            "valu_busy_frac": d.get("valu_busy_frac"),
+            "cyc_per_mfma_f64": d.get("cyc_per_mfma_f64"),
+            "mfma_f64_tflops_under_pmc": d.get("mfma_f64_tflops"),
+            "clock_GHz_under_pmc": d.get("clock_GHz"),
+            "launches_averaged": r["dispatches"],
+            "source": os.path.relpath(a.mfma_dir, REPO), "label": a.label,
+            "note": "rocprofv3 --pmc passes (tools/pmc_passes.sh mfma, occ); "
+                    "mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE"
+                    " / 8 x 256 CUs x 4 SIMDs); valu_busy_frac = 4 x "
+                    "SQ_ACTIVE_INST_VALU / same (issue cycles)",
+        }
+        upsert(os.path.join(REPO, "profiles", "mfma.json"), entry)
+        print(json.dumps(entry, indent=1))
 
 
 if __name__ == "__main__":
