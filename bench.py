@@ -56,8 +56,9 @@ def parse():
     ap.add_argument("--ring-gb", type=float, default=16.0,
                     help="HBM ring for the output cubes (GiB)")
     ap.add_argument("--precise-sincos", action="store_true",
-                    help="fp64 sincos epilogue (default: fp64 range reduction "
-                         "+ fp32 sincos, |err| <= 3e-7)")
+                    help="fp64 sincos epilogue (default: exact fp64 reduction "
+                         "of the phase in revolutions + hardware fp32 sincos, "
+                         "|err| <= 2.3e-7)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fits", action="store_true",
                     help="skip the FITS-cube wall-clock leg (configs 1-2)")
@@ -222,7 +223,7 @@ def sampled_slots_check(ctx, torch, dev, setup, coef, N, flags, slot_sums,
                         n_evals, fast, cxx=None, cyy=None):
     """Parity of sampled slots of the timed run (not timed): slots 0, S/2 and
     S-1 evaluated alone vs an fp64 torch restatement of kl_screen.py:444-449
-    (|d| <= 2e-6 with the fp32 sincos epilogue, 1e-6 with fp64), and -- in
+    (|d| <= 2e-6 with the fast sincos epilogue, 1e-6 with fp64), and -- in
     checksum mode -- their cube checksums vs the per-slot sums the streamed
     launches accumulated (n_evals identical evaluations of each slot)."""
     D = coef.shape[1]
@@ -672,6 +673,19 @@ def main():
         }
         if side:
             line["side_legs"] = side
+        # the fit (slots/s and achieved fp64 FLOP/s): alone
+        # on the whole chip (side leg) and per kernel from PMC passes
+        fe = _profile_entry("fit_flops.json", wkey, "fit")
+        fa = side.get("fit_alone_whole_chip") if side else None
+        if fa or fe:
+            line["fit"] = {
+                "slots_per_s_alone": fa["slots_per_s"] if fa else None,
+                "ms_per_step_in_pipeline": t_fit * 1e3,
+                "fp64_peak_tflops": FP64_MFMA_PEAK_TFS,
+                "kernels_pmc": {k: {"fp64_tflops": v.get("fp64_tflops"),
+                                    "avg_ms": v.get("avg_ms_under_pmc")}
+                                for k, v in (fe or {}).get("kernels", {}).items()},
+            }
         if not args.no_fits and world == 1:
             line["fits_wallclock"] = fits_wallclock()
         if not args.no_cpu_baseline and world == 1:

@@ -63,8 +63,10 @@ extern "C" {
 
 /* sf_kl_eval flags */
 #define SF_EVAL_NAN_SCRUB 1u /* NaN -> 1 (real planes), 0 (imag) (screen.py:368-378) */
-#define SF_EVAL_FAST_SINCOS (1u << 8) /* fp64 range reduction + fp32 sincos
-                                         (|err| <= 3e-7) instead of fp64 sincos */
+#define SF_EVAL_FAST_SINCOS (1u << 8) /* exact fp64 reduction of the phase in
+                                         revolutions + hardware fp32 sincos
+                                         (|err| <= 2.3e-7) instead of fp64
+                                         sincos */
 #define SF_EVAL_NT_STORES (1u << 9) /* non-temporal (streaming) cube stores */
 #define SF_EVAL_BIG_ENDIAN (1u << 10) /* store big-endian float32 (the FITS
                                          byte order), for direct file writes */

@@ -1,0 +1,670 @@
+// kl_eval_impl.h -- the evaluation kernels and their launch templates,
+// shared by kl_eval.hip (pixel basis, kernel choice, dispatch on the k-step
+// count) and the kl_eval_ks*.hip units that instantiate launch_eval_pick<KS>
+// for a few KS each, so the five units compile in parallel.  See kl_eval.hip
+// for the design notes.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <type_traits>
+
+#include "sf_internal.h"
+
+namespace sf {
+
+typedef double v4d __attribute__((ext_vector_type(4)));
+
+
+
+// f64 16x16x4 accumulator layout on gfx950: lane l, register r holds
+// D[row = (l >> 4) + 4 r][col = l & 15] (cdna_hip_programming.md §3).
+__device__ __forceinline__ int acc_row(int l, int r) { return (l >> 4) + 4 * r; }
+
+// Fast epilogue (SF_EVAL_FAST_SINCOS): the contraction runs on coefficients
+// pre-scaled by 1 / 2 pi, so it yields the phase in REVOLUTIONS; the fp64
+// reduction rev - rint(rev) to [-1/2, 1/2] is exact, the result is rounded to
+// float (<= 1.5e-8 rev = 9.4e-8 rad) and fed to the hardware v_sin_f32 /
+// v_cos_f32, whose argument is in revolutions (max |err| 1.25e-7 over
+// [-1/2, 1/2] measured on MI355X, profiles/round2a_coexec_probe.txt): ~7 VALU
+// issues per value instead of the ~25 of a polynomial sincos.  On gfx950 the
+// fp64 MFMA holds the SIMD's VALU for its whole 64 cycles (same probe: MFMA
+// and VALU waves on one SIMD take the SUM of their times), so every VALU
+// cycle of the epilogue adds to the contraction's.
+constexpr double kInv2Pi = 0.15915494309189535;
+
+// fp32 revolutions in [-1/2, 1/2] of a phase given in revolutions; NaN / Inf
+// -> 0 when scrubbing, i.e. cos 1 and sin 0 (screen.py:368-378 NaN scrub)
+__device__ __forceinline__ float rev_reduce(double rev, bool scrub) {
+  const float f = (float)(rev - rint(rev));
+  return (scrub && __builtin_isnan(f)) ? 0.0f : f;
+}
+
+// v_sin_f32 / v_cos_f32 return NaN for a NaN argument (checked by the
+// unscrubbed cases of tests/test_gpu_parity.py::test_eval_kernels_agree)
+__device__ __forceinline__ void sincos_rev(float f, float& s, float& c) {
+  s = __builtin_amdgcn_sinf(f);
+  c = __builtin_amdgcn_cosf(f);
+}
+
+// MFMA A fragments of a 16-slot group: lane l holds coef[s0 + (l & 15)]
+// [4 kk + (l >> 4)] for every k-step (0 past S or D), times `scale`.  The
+// loads are unconditional (clamped addresses, then a select), so all KS of
+// them are in flight together: a guarded load compiles to a branch around
+// it and a wait after it, i.e. KS serial round trips to L2 per group.
+template <int KS>
+__device__ __forceinline__ void load_coef(double (&af)[KS],
+                                          const double* __restrict__ coef,
+                                          int64_t s0, int64_t S, int D, int l,
+                                          double scale) {
+  const int64_t s = s0 + (l & 15);
+  const bool srow = s < S;
+  const double* row = coef + (srow ? s : S - 1) * D;
+  double v[KS];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) {
+    const int d = 4 * kk + (l >> 4);
+    v[kk] = row[d < D ? d : D - 1];
+  }
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) {
+    const int d = 4 * kk + (l >> 4);
+    af[kk] = (srow && d < D) ? v[kk] * scale : 0.0;
+  }
+}
+
+// Workgroup index -> (pixel block, slot chunk).  XCD-aware when the pixel
+// blocks divide by 8: consecutive workgroups go to the 8 XCDs round-robin,
+// so XCD x owns pixel blocks [x*per, (x+1)*per) -- or, with the interleaved
+// map (SF_OPT_EVAL_XCD_MAP), pb = x (mod 8) -- and their Cpix slices stay
+// in its L2.  The eval kernels walk bb = blockIdx.x, += gridDim.x (a
+// multiple of 8, so a workgroup stays on its XCD's pixel blocks): one HSA
+// dispatch counts at most 2^32 work-items, which config 5 (16 M slots per
+// GPU at 512^2) would exceed with one workgroup per (pixel block, chunk).
+// Internal flag bit (never set by callers: sf_kl_eval masks it): XCD x takes
+// the pixel blocks pb = x (mod 8) instead of a contiguous eighth.
+constexpr unsigned kEvalXcdInterleave = 1u << 30;
+
+__device__ __forceinline__ void eval_block(int64_t bb, int64_t n_pb,
+                                           int64_t& pb, int64_t& sc,
+                                           unsigned flags) {
+  if ((n_pb & 7) == 0) {
+    const int64_t per = n_pb >> 3;
+    const int64_t x = bb & 7, i = bb >> 3;
+    pb = (flags & kEvalXcdInterleave) ? (i % per) * 8 + x : x * per + (i % per);
+    sc = i / per;
+  } else {
+    pb = bb % n_pb;
+    sc = bb / n_pb;
+  }
+}
+
+// FAST: ph in revolutions (see rev_reduce); else ph in radians, fp64 sincos
+template <bool FAST>
+__device__ __forceinline__ void jones_sincos(double ph, float& s, float& c,
+                                             bool scrub) {
+  if (FAST) {
+    sincos_rev(rev_reduce(ph, scrub), s, c);
+  } else {
+    double sd, cd;
+    sincos(ph, &sd, &cd);
+    s = (float)sd;
+    c = (float)cd;
+  }
+}
+
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef float v2f __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float bswapf(float x) {
+  return __uint_as_float(__builtin_bswap32(__float_as_uint(x)));
+}
+
+// Per-slot output checksum (sf_kl_eval_sums): the sum, mod 2^32, of the
+// 32-bit words the slot's cube holds (as stored: after the NaN scrub and any
+// byte swap).  Integer adds commute, so the value does not depend on which
+// lanes / waves / workgroups contribute in which order.  32-bit wrap-around
+// adds (v_add3_u32 chains) keep the epilogue cost at ~0.5 VALU op per word.
+__device__ __forceinline__ unsigned fbits(float x) { return __float_as_uint(x); }
+
+// Sum over the 16 lanes of each DPP row (every lane of the row receives it):
+// VALU-only butterflies, no LDS round trips.
+__device__ __forceinline__ unsigned row_sum16(unsigned v) {
+  v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad [1,0,3,2]
+  v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad [2,3,0,1]
+  v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false);  // row_ror:4
+  v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+  return v;
+}
+
+template <bool NT>
+__device__ __forceinline__ void store4(float* p, v4f v) {
+  if (NT) __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(p));
+  else *reinterpret_cast<v4f*>(p) = v;
+}
+
+// amplitude screens are log10 values: 10 ** screen (kl_screen.py:338-365);
+// fast path: the XX / YY coefficients are pre-scaled by log2(10), so the
+// contraction gives log2 A, rounded to float for v_exp_f32 (1 ulp)
+constexpr double kLog2of10 = 3.321928094887362;
+__device__ __forceinline__ float amp2f(double log2a) {
+  return __builtin_amdgcn_exp2f((float)log2a);
+}
+
+// SHB ("shared B"): the 4 waves of a workgroup share ONE 64-pixel block,
+// whose Cpix fragments sit in LDS (KS x 2 KiB) instead of 8*KS registers per
+// wave, and take its 16-slot groups round-robin -- the register tile at
+// ~half the VGPRs, so large D (config 5: D = 50) runs 4 waves per SIMD
+// without spilling; same MFMA operands in the same order, same bits.
+template <int KS, int MINW, bool VEC4, bool FAST, bool NT, bool GAIN,
+          bool SHB = false>
+__global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
+    const double* __restrict__ cfrag, const double* __restrict__ coef,
+    const double* __restrict__ coef_xx, const double* __restrict__ coef_yy,
+    int D, int64_t S, int64_t P, int64_t n_pb, int64_t n_sc, int chunk_groups,
+    float* __restrict__ out, int64_t ring, unsigned flags,
+    unsigned* __restrict__ sums) {
+  constexpr int kFrag = KS * kTiles * 64;  // Cpix doubles of a wave pixel block
+  __shared__ double bsh[SHB ? kFrag : 1];
+  const int l = threadIdx.x & 63;
+  // wave index, wave-uniform: keeps slot / ring arithmetic on the SALU
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // XCD-aware block -> (pixel block, slot chunk); SHB: n_pb counts 64-pixel
+  // wave blocks, else 256-pixel workgroup blocks
+  const int64_t n_blocks = n_pb * n_sc;
+  for (int64_t bb = blockIdx.x; bb < n_blocks; bb += gridDim.x) {
+    int64_t pb, sc;
+    eval_block(bb, n_pb, pb, sc, flags);
+    if (sc >= n_sc) continue;  // uniform per workgroup
+    const int64_t wpb = SHB ? pb : pb * kEvalWaves + w;
+    const int64_t p0 = wpb * kWavePix + (int64_t)(l & 15) * kTiles;
+    if constexpr (SHB) {
+      __syncthreads();  // the previous item's reads of bsh are done
+      if (wpb * kWavePix < P)
+        for (int i = threadIdx.x; i < kFrag; i += 256) bsh[i] = cfrag[wpb * kFrag + i];
+      __syncthreads();
+    }
+    if (wpb * kWavePix >= P) continue;
+
+    double bf[SHB ? 1 : KS][kTiles];
+    if constexpr (!SHB) {
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+        for (int t = 0; t < kTiles; ++t)
+          bf[kk][t] = cfrag[((wpb * KS + kk) * kTiles + t) * 64 + l];
+    }
+    auto bval = [&](int kk, int t) -> double {
+      if constexpr (SHB) return bsh[(kk * kTiles + t) * 64 + l];
+      else return bf[kk][t];
+    };
+
+    const bool scrub = flags & SF_EVAL_NAN_SCRUB;
+    const bool be = flags & SF_EVAL_BIG_ENDIAN;
+    const int64_t slot_base = sc * (int64_t)chunk_groups * 16;
+    for (int g = SHB ? w : 0; g < chunk_groups; g += SHB ? kEvalWaves : 1) {
+      const int64_t s0 = slot_base + (int64_t)g * 16;
+      if (s0 >= S) break;
+      // SHB: keep the Cpix reads inside the loop (in LDS, not hoisted into
+      // registers, which is the point)
+      if constexpr (SHB) asm volatile("" ::: "memory");
+      double af[KS];
+      load_coef<KS>(af, coef, s0, S, D, l, FAST ? kInv2Pi : 1.0);
+      // gain: the XX / YY coefficient loads go out with the phase ones
+      double ax[GAIN ? KS : 1], ay[GAIN ? KS : 1];
+      if constexpr (GAIN) {
+        load_coef<KS>(ax, coef_xx, s0, S, D, l, FAST ? kLog2of10 : 1.0);
+        load_coef<KS>(ay, coef_yy, s0, S, D, l, FAST ? kLog2of10 : 1.0);
+      }
+      // ring slot of the group's first slot (S, ring < 2^31: launch_eval);
+      // the 16 rows follow it with at most one wrap when the ring is >= 16
+      // slots -- scalar, no per-lane 64-bit modulo
+      const uint32_t ring0 = (uint32_t)s0 % (uint32_t)ring;
+      v4d acc[kTiles];
+#pragma unroll
+      for (int t = 0; t < kTiles; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+        for (int t = 0; t < kTiles; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[kk], bval(kk, t),
+                                                        acc[t], 0, 0, 0);
+      // gain: the XX / YY log-amplitude screens share the pixel basis
+      v4d accx[GAIN ? kTiles : 1], accy[GAIN ? kTiles : 1];
+      if constexpr (GAIN) {
+#pragma unroll
+        for (int t = 0; t < kTiles; ++t) {
+          accx[t] = v4d{0.0, 0.0, 0.0, 0.0};
+          accy[t] = v4d{0.0, 0.0, 0.0, 0.0};
+        }
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+          for (int t = 0; t < kTiles; ++t) {
+            accx[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ax[kk], bval(kk, t), accx[t], 0, 0, 0);
+            accy[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ay[kk], bval(kk, t), accy[t], 0, 0, 0);
+          }
+      }
+      // one MFMA accumulator row: 4 slot rows x this lane's 4 pixels; BE
+      // (FITS byte order) as a compile-time branch of the whole row
+      auto row_out = [&](int r, auto be_tag) {
+        constexpr bool kBE = decltype(be_tag)::value;
+        const int row = acc_row(l, r);
+        const int64_t s = s0 + row;
+        if (s >= S) return;  // uniform over the 16 lanes of a slot row
+        uint32_t so = ring0 + (uint32_t)row;
+        if (ring >= 16) {
+          if (so >= (uint32_t)ring) so -= (uint32_t)ring;
+        } else {
+          so %= (uint32_t)ring;
+        }
+        // planes 0..3 = Re XX, Im XX, Re YY, Im YY
+        float pv[4][kTiles];
+#pragma unroll
+        for (int t = 0; t < kTiles; ++t) {
+          float sf, cf;
+          if (GAIN) {
+            // a NaN phase stays NaN through A * cos and is scrubbed below,
+            // as the reference scrubs the product (screen.py:368-378)
+            jones_sincos<FAST>(acc[t][r], sf, cf, false);
+            if (FAST) {
+              // fp32 amplitude x fp32 cos / sin: within 2e-6 x max(1, A)
+              const float ax = amp2f(accx[t][r]);
+              const float ay = amp2f(accy[t][r]);
+              pv[0][t] = ax * cf;
+              pv[1][t] = ax * sf;
+              pv[2][t] = ay * cf;
+              pv[3][t] = ay * sf;
+            } else {
+              // reference: A (fp64) * cos (fp64), one cast at the FITS store
+              const double ax = exp10(accx[t][r]);
+              const double ay = exp10(accy[t][r]);
+              pv[0][t] = (float)(ax * (double)cf);
+              pv[1][t] = (float)(ax * (double)sf);
+              pv[2][t] = (float)(ay * (double)cf);
+              pv[3][t] = (float)(ay * (double)sf);
+            }
+          } else {
+            // FAST: NaN scrubbed on the reduced argument (cos 1, sin 0)
+            jones_sincos<FAST>(acc[t][r], sf, cf, scrub);
+            pv[0][t] = pv[2][t] = cf;
+            pv[1][t] = pv[3][t] = sf;
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (scrub && (GAIN || !FAST) && isnan(pv[q][t]))
+              pv[q][t] = (q & 1) ? 0.0f : 1.0f;
+            if (kBE) pv[q][t] = bswapf(pv[q][t]);
+          }
+        }
+        float* o = out + ((int64_t)so * 4) * P + p0;
+        unsigned cs = 0u;
+        if (VEC4) {
+          // P % 4 == 0: a lane's 4 pixels are all inside the grid or all out
+          // (the last wave block of a grid that is not a multiple of 64)
+          if (p0 < P) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const v4f v = {pv[q][0], pv[q][1], pv[q][2], pv[q][3]};
+              store4<NT>(o + q * P, v);
+            }
+            if (sums) {
+              // phase screens store (cos, sin) twice: sum the planes once
+#pragma unroll
+              for (int q = 0; q < (GAIN ? 4 : 2); ++q)
+#pragma unroll
+                for (int t = 0; t < kTiles; ++t) cs += fbits(pv[q][t]);
+              if (!GAIN) cs *= 2u;
+            }
+          }
+        } else {
+#pragma unroll
+          for (int t = 0; t < kTiles; ++t) {
+            if (p0 + t < P) {
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                o[q * P + t] = pv[q][t];
+                if (sums) cs += fbits(pv[q][t]);
+              }
+            }
+          }
+        }
+        if (sums) {
+          // the 16 lanes of this slot row (one DPP row) hold its 64 pixels
+          cs = row_sum16(cs);
+          if ((l & 15) == 0) atomicAdd(sums + s, cs);
+        }
+      };
+      if (be) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) row_out(r, std::true_type{});
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) row_out(r, std::false_type{});
+      }
+    }
+  }  // workgroup walk
+}
+
+// LDS-staged variant (phase screens, fast sincos epilogue): the same MFMA
+// contraction, but the stores are re-mapped so that one wave writes long
+// contiguous runs.  A workgroup of NW waves covers RUN = 64*NW consecutive
+// pixels; per 16-slot group every wave drops its 16 x 64 reduced phases
+// (rev_reduce: fp32 revolutions, exactly the value the register-tile
+// kernel feeds to v_sin / v_cos) into LDS, and after one
+// barrier wave w takes slots w*16/NW.. and, per slot, sweeps the RUN pixels
+// plane by plane: RUN*4 contiguous bytes per (slot, plane) instead of 256 B.
+// The LDS tile is double-buffered, so one barrier per group suffices (a
+// wave reaches the barrier of group g only after reading group g-1).
+// TPW = MFMA tiles per wave: 4 (the wave owns a whole 64-pixel block, as in
+// the register-tile kernel) or 2 (two waves share a block, each holding half
+// of its Cpix fragments -- half the registers, for large D).
+template <int NW, int TPW>
+struct EvalLds {
+  static constexpr int kWavesPerBlock = kTiles / TPW;
+  static constexpr int kRun = kWavePix * NW / kWavesPerBlock;  // pixels per workgroup
+  static constexpr int kStride = kRun + 4;      // padded LDS row (floats)
+  static constexpr int kSlotsPerWave = 16 / NW;
+  static constexpr int kChunks = kRun / 256;    // 1-KiB store runs per plane
+  static_assert(kRun % 256 == 0 && 16 % NW == 0, "bad LDS eval shape");
+};
+
+template <int KS, int NW, int TPW, bool NT>
+__global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
+    const double* __restrict__ cfrag, const double* __restrict__ coef, int D,
+    int ks_real, int64_t S, int64_t P, int64_t n_pb, int64_t n_sc,
+    int chunk_groups, float* __restrict__ out, int64_t ring, unsigned flags,
+    int sleep, unsigned* __restrict__ sums) {
+  using L = EvalLds<NW, TPW>;
+  __shared__ float tile[2][16][L::kStride];
+  const int l = threadIdx.x & 63;
+  // wave index, wave-uniform: keeps slot / ring arithmetic on the SALU
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t n_blocks = n_pb * n_sc;
+  for (int64_t bb = blockIdx.x; bb < n_blocks; bb += gridDim.x) {
+    int64_t pb, sc;
+    eval_block(bb, n_pb, pb, sc, flags);
+    if (sc >= n_sc) continue;  // uniform per workgroup
+    const int wblk = w / L::kWavesPerBlock;         // 64-pixel block in the run
+    const int t0 = (w % L::kWavesPerBlock) * TPW;   // first tile of this wave
+    const int64_t wpb = pb * (NW / L::kWavesPerBlock) + wblk;
+    const bool live = wpb * kWavePix < P;  // waves past the grid still sync
+
+    double bf[KS][TPW];
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+      for (int t = 0; t < TPW; ++t)
+        bf[kk][t] = (live && kk < ks_real)
+                        ? cfrag[((wpb * ks_real + kk) * kTiles + t0 + t) * 64 + l]
+                        : 0.0;
+
+    const bool scrub = flags & SF_EVAL_NAN_SCRUB;
+    const bool be = flags & SF_EVAL_BIG_ENDIAN;
+    const int64_t pix0 = pb * L::kRun;
+    const int64_t slot_base = sc * (int64_t)chunk_groups * 16;
+    for (int g = 0; g < chunk_groups; ++g) {
+      const int64_t s0 = slot_base + (int64_t)g * 16;
+      if (s0 >= S) break;  // uniform per workgroup
+      float(*buf)[L::kStride] = tile[g & 1];
+      // ---- contraction: 16 slots x this wave's 64 pixels
+      double af[KS];
+      load_coef<KS>(af, coef, s0, S, D, l, kInv2Pi);
+      v4d acc[TPW];
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+        for (int t = 0; t < TPW; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[kk], bf[kk][t],
+                                                        acc[t], 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float red[TPW];
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) red[t] = rev_reduce(acc[t][r], scrub);
+        float* dst = &buf[acc_row(l, r)][wblk * kWavePix + (l & 15) * kTiles + t0];
+        if (TPW == 4)
+          *reinterpret_cast<v4f*>(dst) = v4f{red[0], red[1], red[2 % TPW], red[3 % TPW]};
+        else
+          *reinterpret_cast<v2f*>(dst) = v2f{red[0], red[1 % TPW]};
+      }
+      for (int z = 0; z < sleep; ++z) __builtin_amdgcn_s_sleep(1);
+      __syncthreads();
+      // ---- stores: wave w owns kSlotsPerWave slots of the group
+      // BE (FITS byte order) as a compile-time branch of a whole slot
+      auto slot_out = [&](int j, auto be_tag) {
+        constexpr bool kBE = decltype(be_tag)::value;
+        const int row = w * L::kSlotsPerWave + j;
+        const int64_t s = s0 + row;
+        if (s >= S) return;  // uniform per wave
+        float cv[L::kChunks][4], sv[L::kChunks][4];
+#pragma unroll
+        for (int c = 0; c < L::kChunks; ++c) {
+          const v4f rv = *reinterpret_cast<const v4f*>(&buf[row][c * 256 + 4 * l]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float sn, cs;
+            sincos_rev(rv[e], sn, cs);
+            if (kBE) {
+              cs = bswapf(cs);
+              sn = bswapf(sn);
+            }
+            cv[c][e] = cs;
+            sv[c][e] = sn;
+          }
+        }
+        // S, ring < 2^31 (launch_eval): 32-bit scalar modulo
+        const int64_t so = (uint32_t)s % (uint32_t)ring;
+        float* o = out + (so * 4) * P + pix0 + 4 * l;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+#pragma unroll
+          for (int c = 0; c < L::kChunks; ++c) {
+            if (pix0 + c * 256 + 4 * l < P) {
+              const v4f v = (q & 1) ? v4f{sv[c][0], sv[c][1], sv[c][2], sv[c][3]}
+                                    : v4f{cv[c][0], cv[c][1], cv[c][2], cv[c][3]};
+              store4<NT>(o + q * P + c * 256, v);
+            }
+          }
+        }
+        if (sums) {
+          // planes 0 / 2 hold cos, 1 / 3 sin: every value is stored twice
+          unsigned cs = 0u;
+#pragma unroll
+          for (int c = 0; c < L::kChunks; ++c)
+            if (pix0 + c * 256 + 4 * l < P)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) cs += fbits(cv[c][e]) + fbits(sv[c][e]);
+          cs = row_sum16(2u * cs);
+          // the 4 row totals, uniform (scalar) values
+          const unsigned tot = (unsigned)__builtin_amdgcn_readlane((int)cs, 0) +
+                               (unsigned)__builtin_amdgcn_readlane((int)cs, 16) +
+                               (unsigned)__builtin_amdgcn_readlane((int)cs, 32) +
+                               (unsigned)__builtin_amdgcn_readlane((int)cs, 48);
+          if (l == 0) atomicAdd(sums + s, tot);
+        }
+      };
+      if (be) {
+#pragma unroll
+        for (int j = 0; j < L::kSlotsPerWave; ++j) slot_out(j, std::true_type{});
+      } else {
+#pragma unroll
+        for (int j = 0; j < L::kSlotsPerWave; ++j) slot_out(j, std::false_type{});
+      }
+    }
+    // the next workgroup item reuses the LDS tiles from buffer 0
+    __syncthreads();
+  }  // workgroup walk
+}
+
+// Grid of an eval launch: one workgroup per (pixel block, slot chunk) up to
+// the dispatch limit of 2^32 work-items (kept at 2^31), a multiple of 8 so
+// the XCD mapping of eval_block holds for every item a workgroup walks.
+inline int64_t eval_grid(const sf_ctx* ctx, int64_t n_pb, int64_t n_sc,
+                         int threads) {
+  int64_t n = n_pb * n_sc;
+  if ((n_pb & 7) == 0) n = ((n + 7) / 8) * 8;
+  int64_t cap = ((int64_t)1 << 31) / threads;
+  if (ctx->eval_max_blocks > 0 && ctx->eval_max_blocks < cap)
+    cap = ctx->eval_max_blocks;
+  cap = cap < 8 ? 8 : cap & ~(int64_t)7;
+  return n < cap ? n : cap;
+}
+
+// 16-slot groups per (pixel block, slot chunk) work item: as many as keep
+// >= min_items items (the grid fills the chip), at most max_groups
+// (SF_OPT_EVAL_GROUPS, else 64 for the register tile, 16 for the LDS-staged
+// kernels).  Every item loads its pixel block's Cpix fragments once, so long
+// chunks keep that reload small against the item's output: at 512^2 x D = 50
+// the Cpix of one XCD's pixel blocks (13.6 MB) outgrows its 4 MiB L2, and 16
+// groups per item re-read 3.6 TB of it per 8.2 M-slot launch (FETCH_SIZE,
+// 10 % of the writes; 64 groups: 0.9 TB, +2 %); at 256^2 x D = 20 the slices
+// stay in L2 and 16 groups keep each XCD's coefficient rows there too
+// (profiles/round2e_eval_groups_ab.txt, round2f_eval_groups_bench.txt).
+inline int eval_chunk_groups(int64_t n_pb, int64_t S, int max_groups,
+                             int64_t min_items) {
+  int groups = max_groups;
+  while (groups > 1 && n_pb * ((S + 16 * groups - 1) / (16 * groups)) < min_items)
+    groups >>= 1;
+  return groups;
+}
+
+
+template <int KS, int MINW>
+int launch_eval_ks(sf_ctx* ctx, const double* coef,
+                          const double* cxx, const double* cyy, int64_t S,
+                          float* out, int64_t ring, unsigned flags,
+                          unsigned* sums) {
+  const int64_t P = ctx->n_pix;
+  const int64_t n_pb = ctx->n_pix_blocks;
+  const int groups = eval_chunk_groups(n_pb, S, ctx->eval_groups ? ctx->eval_groups : 64, 2048);
+  const int64_t n_sc = (S + 16 * groups - 1) / (16 * groups);
+  const int64_t nblk = eval_grid(ctx, n_pb, n_sc, 256);
+  const bool vec4 = (P % 4 == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
+  const bool fast = flags & SF_EVAL_FAST_SINCOS;
+  const bool nt = flags & SF_EVAL_NT_STORES;
+  const bool gain = cxx != nullptr;
+#define SF_LAUNCH(V, F, N, G)                                                 \
+  hipLaunchKernelGGL((kl_eval_kernel<KS, MINW, V, F, N, G>), dim3((unsigned)nblk),  \
+                     dim3(256), 0, ctx->stream, ctx->d_cfrag, coef, cxx, cyy, \
+                     ctx->D, S, P, n_pb, n_sc, groups, out, ring, flags, sums)
+#define SF_LAUNCH_G(V, F, N) \
+  do {                       \
+    if (gain)                \
+      SF_LAUNCH(V, F, N, true); \
+    else                     \
+      SF_LAUNCH(V, F, N, false); \
+  } while (0)
+  if (vec4) {
+    if (fast) {
+      if (nt) SF_LAUNCH_G(true, true, true); else SF_LAUNCH_G(true, true, false);
+    } else {
+      if (nt) SF_LAUNCH_G(true, false, true); else SF_LAUNCH_G(true, false, false);
+    }
+  } else {
+    if (fast) SF_LAUNCH_G(false, true, false); else SF_LAUNCH_G(false, false, false);
+  }
+#undef SF_LAUNCH_G
+#undef SF_LAUNCH
+  SF_HIP(hipGetLastError());
+  return SF_OK;
+}
+
+// SHB register tile (phase screens, float4-aligned output): one workgroup
+// per (64-pixel wave block, chunk of 4 x 16 groups of 16 slots)
+template <int KS>
+int launch_eval_shb(sf_ctx* ctx, const double* coef, int64_t S,
+                           float* out, int64_t ring, unsigned flags,
+                           unsigned* sums) {
+  const int64_t P = ctx->n_pix;
+  const int64_t n_wpb = ctx->n_pix_blocks * kEvalWaves;
+  const int groups = eval_chunk_groups(n_wpb, S, ctx->eval_groups ? ctx->eval_groups : 64, 4096);
+  const int64_t n_sc = (S + 16 * groups - 1) / (16 * groups);
+  const int64_t nblk = eval_grid(ctx, n_wpb, n_sc, 256);
+  const bool fast = flags & SF_EVAL_FAST_SINCOS;
+  const bool nt = flags & SF_EVAL_NT_STORES;
+#define SF_LAUNCH_SHB(F, N)                                                     \
+  hipLaunchKernelGGL((kl_eval_kernel<KS, 4, true, F, N, false, true>),          \
+                     dim3((unsigned)nblk), dim3(256), 0, ctx->stream,           \
+                     ctx->d_cfrag, coef, nullptr, nullptr, ctx->D, S, P, n_wpb, \
+                     n_sc, groups, out, ring, flags, sums)
+  if (fast) {
+    if (nt) SF_LAUNCH_SHB(true, true); else SF_LAUNCH_SHB(true, false);
+  } else {
+    if (nt) SF_LAUNCH_SHB(false, true); else SF_LAUNCH_SHB(false, false);
+  }
+#undef SF_LAUNCH_SHB
+  SF_HIP(hipGetLastError());
+  return SF_OK;
+}
+
+template <int KS, int NW, int TPW>
+int launch_eval_lds(sf_ctx* ctx, const double* coef, int64_t S,
+                           float* out, int64_t ring, unsigned flags,
+                           unsigned* sums) {
+  const int64_t P = ctx->n_pix;
+  const int64_t run = EvalLds<NW, TPW>::kRun;
+  const int64_t n_pb = (P + run - 1) / run;
+  const int groups = eval_chunk_groups(n_pb, S, ctx->eval_groups ? ctx->eval_groups : 16, 1024);
+  const int64_t n_sc = (S + 16 * groups - 1) / (16 * groups);
+  const int64_t nblk = eval_grid(ctx, n_pb, n_sc, 64 * NW);
+  // auto XCD map: interleave the pixel blocks over the XCDs when each XCD's
+  // contiguous eighth would be <= 8 blocks (measured: 256^2 at 4 KiB runs
+  // +2-3 %, 512^2 -3 %; profiles/round1e_eval_xcd_map.txt)
+  if (ctx->eval_xcd_map < 0 && (n_pb & 7) == 0 && n_pb / 8 <= 8)
+    flags |= kEvalXcdInterleave;
+  if (flags & SF_EVAL_NT_STORES)
+    hipLaunchKernelGGL((kl_eval_lds_kernel<KS, NW, TPW, true>), dim3((unsigned)nblk),
+                       dim3(64 * NW), 0, ctx->stream, ctx->d_cfrag, coef, ctx->D,
+                       ctx->ksteps, S, P, n_pb, n_sc, groups, out, ring, flags,
+                       ctx->eval_sleep, sums);
+  else
+    hipLaunchKernelGGL((kl_eval_lds_kernel<KS, NW, TPW, false>), dim3((unsigned)nblk),
+                       dim3(64 * NW), 0, ctx->stream, ctx->d_cfrag, coef, ctx->D,
+                       ctx->ksteps, S, P, n_pb, n_sc, groups, out, ring, flags,
+                       ctx->eval_sleep, sums);
+  SF_HIP(hipGetLastError());
+  return SF_OK;
+}
+
+
+template <int KS>
+int launch_eval_pick(sf_ctx* ctx, const double* coef, const double* cxx,
+                            const double* cyy, int64_t S, float* out,
+                            int64_t ring, unsigned flags,
+                            unsigned* sums) {
+  const int v = pick_eval_kernel(ctx, cxx != nullptr, flags,
+                                 (reinterpret_cast<uintptr_t>(out) & 15) == 0);
+  switch (v) {
+    case SF_EVAL_KERNEL_LDS4:
+      return launch_eval_lds<KS, 4, 4>(ctx, coef, S, out, ring, flags, sums);
+    case SF_EVAL_KERNEL_LDS8:
+      return launch_eval_lds<KS, 8, 4>(ctx, coef, S, out, ring, flags, sums);
+    case SF_EVAL_KERNEL_LDS16:
+      return launch_eval_lds<KS, 16, 4>(ctx, coef, S, out, ring, flags, sums);
+    case SF_EVAL_KERNEL_LDS8H:
+      return launch_eval_lds<KS, 8, 2>(ctx, coef, S, out, ring, flags, sums);
+    case SF_EVAL_KERNEL_LDS16H:
+      return launch_eval_lds<KS, 16, 2>(ctx, coef, S, out, ring, flags, sums);
+    case SF_EVAL_KERNEL_SHB:
+      return launch_eval_shb<KS>(ctx, coef, S, out, ring, flags, sums);
+    case SF_EVAL_KERNEL_TILE3:
+      // below 8 k-steps the register tile fits 4 waves/SIMD anyway
+      return launch_eval_ks<KS, (KS >= 8 ? 3 : 2)>(ctx, coef, cxx, cyy, S, out,
+                                                   ring, flags, sums);
+    default:
+      return launch_eval_ks<KS, 2>(ctx, coef, cxx, cyy, S, out, ring, flags, sums);
+  }
+}
+
+#define SF_EVAL_PICK_ARGS                                                    \
+  sf_ctx* ctx, const double* coef, const double* cxx, const double* cyy,   \
+      int64_t S, float* out, int64_t ring, unsigned flags, unsigned* sums
+#define SF_EVAL_KS_LIST(X) \
+  X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15)
+#define SF_EVAL_EXTERN(k) extern template int launch_eval_pick<k>(SF_EVAL_PICK_ARGS);
+#define SF_EVAL_INSTANTIATE(k) template int launch_eval_pick<k>(SF_EVAL_PICK_ARGS);
+
+}  // namespace sf

@@ -58,6 +58,8 @@ def main():
     ap.add_argument("--coef-sets", type=int, default=1, help="3 for gain screens")
     ap.add_argument("--eval-kernel", required=True,
                     help="bench.py's roofline.kernel for the profiled run")
+    ap.add_argument("--fit-dir", help="pmc_passes.sh dir with valu/ occ/ of a "
+                    "fit + eval run: fp64 FLOP/s of the fit kernels")
     ap.add_argument("--label", default="")
     a = ap.parse_args()
     algo = a.slots * (16 * a.grid * a.grid + 8 * a.n_dir * a.coef_sets)
@@ -78,6 +80,10 @@ def main():
         }
         upsert(os.path.join(REPO, "profiles", "traffic.json"), entry)
         print(json.dumps(entry, indent=1))
+    if a.fit_dir:
+        entry = fit_entry(a.fit_dir, a.workload, a.label)
+        upsert(os.path.join(REPO, "profiles", "fit_flops.json"), entry)
+        print(json.dumps(entry, indent=1))
     if a.mfma_dir:
         r = summary(a.mfma_dir, a.kernel)
         d = r["derived"]
@@ -97,6 +103,29 @@ def main():
         }
         upsert(os.path.join(REPO, "profiles", "mfma.json"), entry)
         print(json.dumps(entry, indent=1))
+
+
+def fit_entry(d, workload, label):
+    """fp64 FLOP/s of the fit kernels (VALU: 64 x (2 FMA + MUL + ADD + TRANS)
+    per wave-instruction, SQ_INSTS_VALU_*_F64; no MFMA in the fit)."""
+    kernels = {}
+    for k in ("kl_fit_pass_kernel", "kl_subset_eig_kernel", "kl_classify_kernel",
+              "kl_assign_kernel", "kl_fit_general_kernel"):
+        try:
+            r = summary(d, k)
+        except subprocess.CalledProcessError:
+            continue
+        dd = r["derived"]
+        kernels[k] = {"kernel": r["kernel"], "dispatches_averaged": r["dispatches"],
+                      "avg_ms_under_pmc": r["avg_ms_under_pmc"],
+                      "fp64_flop_per_launch": dd.get("valu_fp64_flop"),
+                      "fp64_tflops": dd.get("valu_fp64_tflops"),
+                      "valu_busy_frac": dd.get("valu_busy_frac")}
+    return {"workload": workload, "eval_kernel": "fit", "kernels": kernels,
+            "source": os.path.relpath(d, REPO), "label": label,
+            "note": "largest-grid launch of each fit kernel in a bench.py "
+                    "--steps 1 --warmup 0 run under rocprofv3 --pmc (valu, occ "
+                    "passes); fp64 VALU peak 78.6 TFLOP/s"}
 
 
 if __name__ == "__main__":
