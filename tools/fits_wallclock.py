@@ -33,7 +33,13 @@ CASES = {
     # generator as bench.py
     "config3-10t": ("kl", 0.01301, 0.0),
 }
-SYNTH = {"config3-10t": (64, 10, 16, 20)}
+SYNTH = {"config3-10t": (64, 10, 16, 20), "config3": (64, 100, 16, 20)}
+CASES["config3"] = ("kl", 0.01301, 0.0)
+# config 3's whole 107 GB cube does not fit the GPU box's 79 GB disk: it is
+# written as the reference writes a memory-limited cube -- one FITS file per
+# time chunk (screen.py:283-317) -- with 10 times (10.7 GB) per file, and each
+# file is deleted once closed (unlink time reported apart)
+CHUNKED = {"config3": 10}
 
 
 def synthetic_npz(name, outdir):
@@ -54,19 +60,59 @@ def run(name, outdir, h5=None, slots=14880):
     st, cell, smooth = CASES[name]
     outroot = os.path.join(outdir, name)
     sky = SKY if h5 is None else None
-    t0 = time.perf_counter()
-    make_aterm_image(h5 or FIX, soltabname="phase000", screen_type=st,
-                     outroot=outroot,
-                     bounds_deg=[124.565, 66.165, 127.895, 62.835],
-                     bounds_mid_deg=[126.23, 64.50], skymodel=sky,
-                     padding_fraction=0, cellsize_deg=cell, smooth_deg=smooth,
-                     ncpu=0)
-    dt = time.perf_counter() - t0
-    size = sum(os.path.getsize(os.path.join(outdir, f)) for f in os.listdir(outdir)
-               if f.startswith(name) and f.endswith(".fits"))
-    return {"case": name, "screen_type": st, "cellsize_deg": cell,
-            "wall_s": dt, "fits_bytes": size, "slots": slots,
-            "slots_per_s": slots / dt, "fits_GB_per_s": size / dt / 1e9}
+    undo, state = _chunked(name)
+    try:
+        t0 = time.perf_counter()
+        make_aterm_image(h5 or FIX, soltabname="phase000", screen_type=st,
+                         outroot=outroot,
+                         bounds_deg=[124.565, 66.165, 127.895, 62.835],
+                         bounds_mid_deg=[126.23, 64.50], skymodel=sky,
+                         padding_fraction=0, cellsize_deg=cell, smooth_deg=smooth,
+                         ncpu=0)
+        dt = time.perf_counter() - t0
+    finally:
+        undo()
+    size = state["bytes"] + sum(
+        os.path.getsize(os.path.join(outdir, f)) for f in os.listdir(outdir)
+        if f.startswith(name) and f.endswith(".fits"))
+    r = {"case": name, "screen_type": st, "cellsize_deg": cell,
+         "wall_s": dt, "fits_bytes": size, "slots": slots,
+         "slots_per_s": slots / dt, "fits_GB_per_s": size / dt / 1e9}
+    if state["files"]:
+        r.update(files=state["files"], unlink_s=state["unlink_s"],
+                 wall_s_without_unlink=dt - state["unlink_s"],
+                 fits_GB_per_s_without_unlink=size / (dt - state["unlink_s"]) / 1e9)
+    return r
+
+
+def _chunked(name):
+    """For CHUNKED cases: split the time axis every n times (as
+    Screen.write's memory chunking would) and delete each FITS file when its
+    writer closes.  Returns (undo, state)."""
+    state = {"bytes": 0, "files": 0, "unlink_s": 0.0}
+    if name not in CHUNKED:
+        return (lambda: None), state
+    import numpy as np
+    from ska_sdp_screen_fitting_amd import fits, screen
+    n = CHUNKED[name]
+    orig_tc, orig_close = screen.time_chunks, fits.CubeWriter.close
+
+    def time_chunks(times, mem_per_slot_gb, available_gb=None):
+        return list(range(n, len(np.asarray(times)), n)) + [len(np.asarray(times))]
+
+    def close(self):
+        orig_close(self)
+        state["bytes"] += os.path.getsize(self.path)
+        state["files"] += 1
+        t = time.perf_counter()
+        os.remove(self.path)
+        state["unlink_s"] += time.perf_counter() - t
+
+    screen.time_chunks, fits.CubeWriter.close = time_chunks, close
+
+    def undo():
+        screen.time_chunks, fits.CubeWriter.close = orig_tc, orig_close
+    return undo, state
 
 
 def main():
