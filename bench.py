@@ -352,6 +352,18 @@ def side_legs(ctx, torch, dev, stream, fit_stream, fit, evaluate, coef, bounds,
     ms = timed(lambda: fit(0, fit_stream), fit_stream)
     res["fit_alone_whole_chip"] = {"slots": n, "ms": ms,
                                    "slots_per_s": n / ms * 1e3}
+    # the box's store ceiling for context (boxes differ by ~10 %): zero_
+    # (hipMemsetAsync) and fill_ of the whole output ring, on the eval stream
+    flat = out.view(-1)
+    nbytes = flat.numel() * 4
+    best = 0.0
+    with torch.cuda.stream(stream):
+        for fn in (flat.zero_, lambda: flat.fill_(1.0)):
+            best = max(best, nbytes / timed(fn, stream) / 1e6)
+    res["store_ceiling"] = {"GBs": best, "frac_of_peak": best / HBM_PEAK_GBS,
+                            "bytes": nbytes,
+                            "what": "max of zero_ (hipMemsetAsync) and fill_ "
+                                    "over the output ring"}
     ctx.set_stream(stream.cuda_stream)
     return res
 
@@ -622,6 +634,7 @@ def main():
         if (tj is not None and tj.get("flags") == flags
                 and tj.get("chunks", 1) == n_chunks):
             traffic = tj.get("hbm_bytes_per_launch")
+        ceil = side.get("store_ceiling") if side else None
         line = {
             "metric": METRIC,
             "value": T * F * A_total * args.steps / elapsed,
@@ -661,6 +674,7 @@ def main():
                 "kernel": eval_kernel_name,
                 "bytes_per_launch": launch_bytes,
                 "launch_ms": t_eval_launch * 1e3,
+                "frac_of_box_store_ceiling": achieved / ceil["GBs"] if ceil else None,
             },
             "mfma": mfma_line(eval_kernel_name, S / n_chunks, P, D,
                               t_eval_launch, wkey, 3 if gain else 1),

@@ -99,17 +99,48 @@ __device__ __forceinline__ void eval_block(int64_t bb, int64_t n_pb,
   }
 }
 
-// FAST: ph in revolutions (see rev_reduce); else ph in radians, fp64 sincos
+// Precise epilogue (no SF_EVAL_FAST_SINCOS): sin / cos(2 pi rev) in fp64 to
+// ~1e-16, then one cast to float (the reference's fp64 cos / sin cast at the
+// FITS store, Q12).  rev - rint(rev) and the quarter-turn split are exact;
+// the remaining |t| <= 1/8 turn is scaled by 2 pi (relative error 1e-16) and
+// fed to Taylor polynomials to x^15 / x^16 on |x| <= pi/4 (truncation
+// <= 1e-15): ~20 fp64 VALU issues per value instead of ocml's sincos with its
+// large-argument reduction.  NaN / Inf in, NaN out.
+__device__ __forceinline__ void sincos_rev_f64(double rev, float& s, float& c) {
+  const double fr = rev - rint(rev);            // [-1/2, 1/2] turn, exact
+  const double q = rint(fr * 4.0);              // quarter turns, -2..2
+  const double x = fma(-q, 0.25, fr) * 6.283185307179586;  // |x| <= pi/4
+  const double x2 = x * x;
+  double ps = fma(x2, 7.647163731819816e-13, -1.6059043836821613e-10);
+  ps = fma(x2, ps, 2.505210838544172e-08);
+  ps = fma(x2, ps, -2.7557319223985893e-06);
+  ps = fma(x2, ps, 1.984126984126984e-04);
+  ps = fma(x2, ps, -8.333333333333333e-03);
+  ps = fma(x2, ps, 1.6666666666666666e-01);
+  const double sx = fma(-x * x2, ps, x);        // x - x^3 / 6 + ...
+  double pc = fma(x2, -1.1470745597729725e-11, 2.08767569878681e-09);
+  pc = fma(x2, pc, -2.755731922398589e-07);
+  pc = fma(x2, pc, 2.48015873015873e-05);
+  pc = fma(x2, pc, -1.3888888888888889e-03);
+  pc = fma(x2, pc, 4.1666666666666664e-02);
+  pc = fma(x2, pc, -0.5);
+  const double cx = fma(x2, pc, 1.0);           // 1 - x^2 / 2 + ...
+  const int iq = (int)q & 3;
+  const double a = (iq & 1) ? cx : sx;
+  const double b = (iq & 1) ? sx : cx;
+  s = (float)((iq & 2) ? -a : a);
+  c = (float)(((iq + 1) & 2) ? -b : b);
+}
+
+// ph in revolutions (the coefficients are scaled by 1 / 2 pi as loaded):
+// FAST = hardware fp32 sincos (rev_reduce), else sincos_rev_f64
 template <bool FAST>
 __device__ __forceinline__ void jones_sincos(double ph, float& s, float& c,
                                              bool scrub) {
   if (FAST) {
     sincos_rev(rev_reduce(ph, scrub), s, c);
   } else {
-    double sd, cd;
-    sincos(ph, &sd, &cd);
-    s = (float)sd;
-    c = (float)cd;
+    sincos_rev_f64(ph, s, c);
   }
 }
 
@@ -162,7 +193,7 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
     const double* __restrict__ cfrag, const double* __restrict__ coef,
     const double* __restrict__ coef_xx, const double* __restrict__ coef_yy,
     int D, int64_t S, int64_t P, int64_t n_pb, int64_t n_sc, int chunk_groups,
-    float* __restrict__ out, int64_t ring, unsigned flags,
+    float* __restrict__ out, int64_t ring, int64_t ring_base, unsigned flags,
     unsigned* __restrict__ sums) {
   constexpr int kFrag = KS * kTiles * 64;  // Cpix doubles of a wave pixel block
   __shared__ double bsh[SHB ? kFrag : 1];
@@ -209,7 +240,7 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
       // registers, which is the point)
       if constexpr (SHB) asm volatile("" ::: "memory");
       double af[KS];
-      load_coef<KS>(af, coef, s0, S, D, l, FAST ? kInv2Pi : 1.0);
+      load_coef<KS>(af, coef, s0, S, D, l, kInv2Pi);  // phase in turns
       // gain: the XX / YY coefficient loads go out with the phase ones
       double ax[GAIN ? KS : 1], ay[GAIN ? KS : 1];
       if constexpr (GAIN) {
@@ -219,7 +250,7 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
       // ring slot of the group's first slot (S, ring < 2^31: launch_eval);
       // the 16 rows follow it with at most one wrap when the ring is >= 16
       // slots -- scalar, no per-lane 64-bit modulo
-      const uint32_t ring0 = (uint32_t)s0 % (uint32_t)ring;
+      const uint32_t ring0 = (uint32_t)(s0 + ring_base) % (uint32_t)ring;
       v4d acc[kTiles];
 #pragma unroll
       for (int t = 0; t < kTiles; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
@@ -373,7 +404,8 @@ template <int KS, int NW, int TPW, bool NT>
 __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
     const double* __restrict__ cfrag, const double* __restrict__ coef, int D,
     int ks_real, int64_t S, int64_t P, int64_t n_pb, int64_t n_sc,
-    int chunk_groups, float* __restrict__ out, int64_t ring, unsigned flags,
+    int chunk_groups, float* __restrict__ out, int64_t ring, int64_t ring_base,
+    unsigned flags,
     int sleep, unsigned* __restrict__ sums) {
   using L = EvalLds<NW, TPW>;
   __shared__ float tile[2][16][L::kStride];
@@ -456,7 +488,7 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
           }
         }
         // S, ring < 2^31 (launch_eval): 32-bit scalar modulo
-        const int64_t so = (uint32_t)s % (uint32_t)ring;
+        const int64_t so = (uint32_t)(s + ring_base) % (uint32_t)ring;
         float* o = out + (so * 4) * P + pix0 + 4 * l;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -532,24 +564,44 @@ inline int eval_chunk_groups(int64_t n_pb, int64_t S, int max_groups,
 }
 
 
+// Slots per launch that keep one workgroup per work item: the dispatch caps
+// a grid at 2^31 work-items (eval_grid); past that the workgroups would walk
+// several items each, which measured 3-8 % slower than one-shot workgroups
+// dispatched in slot order (profiles/round2k_eval_split.txt), so a call
+// longer than that is split into consecutive launches.
+inline int64_t eval_launch_slots(const sf_ctx* ctx, int64_t n_pb, int groups,
+                                 int threads) {
+  int64_t cap = ((int64_t)1 << 31) / threads;
+  if (ctx->eval_max_blocks > 0) return INT64_MAX;  // the walk test keeps one launch
+  const int64_t chunks = cap / n_pb;
+  return (chunks < 1 ? 1 : chunks) * 16 * groups;
+}
+
 template <int KS, int MINW>
 int launch_eval_ks(sf_ctx* ctx, const double* coef,
-                          const double* cxx, const double* cyy, int64_t S,
+                          const double* cxx, const double* cyy, int64_t S_all,
                           float* out, int64_t ring, unsigned flags,
                           unsigned* sums) {
   const int64_t P = ctx->n_pix;
   const int64_t n_pb = ctx->n_pix_blocks;
-  const int groups = eval_chunk_groups(n_pb, S, ctx->eval_groups ? ctx->eval_groups : 64, 2048);
+  const int groups = eval_chunk_groups(n_pb, S_all, ctx->eval_groups ? ctx->eval_groups : 64, 2048);
+  const int64_t per = eval_launch_slots(ctx, n_pb, groups, 256);
+  for (int64_t b = 0; b < S_all; b += per) {
+  const int64_t S = S_all - b < per ? S_all - b : per;
   const int64_t n_sc = (S + 16 * groups - 1) / (16 * groups);
   const int64_t nblk = eval_grid(ctx, n_pb, n_sc, 256);
+  const double* cb = coef + b * ctx->D;
+  const double* cxb = cxx ? cxx + b * ctx->D : nullptr;
+  const double* cyb = cyy ? cyy + b * ctx->D : nullptr;
+  unsigned* sb = sums ? sums + b : nullptr;
   const bool vec4 = (P % 4 == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
   const bool fast = flags & SF_EVAL_FAST_SINCOS;
   const bool nt = flags & SF_EVAL_NT_STORES;
   const bool gain = cxx != nullptr;
 #define SF_LAUNCH(V, F, N, G)                                                 \
   hipLaunchKernelGGL((kl_eval_kernel<KS, MINW, V, F, N, G>), dim3((unsigned)nblk),  \
-                     dim3(256), 0, ctx->stream, ctx->d_cfrag, coef, cxx, cyy, \
-                     ctx->D, S, P, n_pb, n_sc, groups, out, ring, flags, sums)
+                     dim3(256), 0, ctx->stream, ctx->d_cfrag, cb, cxb, cyb, \
+                     ctx->D, S, P, n_pb, n_sc, groups, out, ring, b % ring, flags, sb)
 #define SF_LAUNCH_G(V, F, N) \
   do {                       \
     if (gain)                \
@@ -569,27 +621,33 @@ int launch_eval_ks(sf_ctx* ctx, const double* coef,
 #undef SF_LAUNCH_G
 #undef SF_LAUNCH
   SF_HIP(hipGetLastError());
+  }
   return SF_OK;
 }
 
 // SHB register tile (phase screens, float4-aligned output): one workgroup
 // per (64-pixel wave block, chunk of 4 x 16 groups of 16 slots)
 template <int KS>
-int launch_eval_shb(sf_ctx* ctx, const double* coef, int64_t S,
+int launch_eval_shb(sf_ctx* ctx, const double* coef, int64_t S_all,
                            float* out, int64_t ring, unsigned flags,
                            unsigned* sums) {
   const int64_t P = ctx->n_pix;
   const int64_t n_wpb = ctx->n_pix_blocks * kEvalWaves;
-  const int groups = eval_chunk_groups(n_wpb, S, ctx->eval_groups ? ctx->eval_groups : 64, 4096);
+  const int groups = eval_chunk_groups(n_wpb, S_all, ctx->eval_groups ? ctx->eval_groups : 64, 4096);
+  const int64_t per = eval_launch_slots(ctx, n_wpb, groups, 256);
+  for (int64_t b = 0; b < S_all; b += per) {
+  const int64_t S = S_all - b < per ? S_all - b : per;
   const int64_t n_sc = (S + 16 * groups - 1) / (16 * groups);
   const int64_t nblk = eval_grid(ctx, n_wpb, n_sc, 256);
+  const double* cb = coef + b * ctx->D;
+  unsigned* sb = sums ? sums + b : nullptr;
   const bool fast = flags & SF_EVAL_FAST_SINCOS;
   const bool nt = flags & SF_EVAL_NT_STORES;
 #define SF_LAUNCH_SHB(F, N)                                                     \
   hipLaunchKernelGGL((kl_eval_kernel<KS, 4, true, F, N, false, true>),          \
                      dim3((unsigned)nblk), dim3(256), 0, ctx->stream,           \
-                     ctx->d_cfrag, coef, nullptr, nullptr, ctx->D, S, P, n_wpb, \
-                     n_sc, groups, out, ring, flags, sums)
+                     ctx->d_cfrag, cb, nullptr, nullptr, ctx->D, S, P, n_wpb, \
+                     n_sc, groups, out, ring, b % ring, flags, sb)
   if (fast) {
     if (nt) SF_LAUNCH_SHB(true, true); else SF_LAUNCH_SHB(true, false);
   } else {
@@ -597,35 +655,49 @@ int launch_eval_shb(sf_ctx* ctx, const double* coef, int64_t S,
   }
 #undef SF_LAUNCH_SHB
   SF_HIP(hipGetLastError());
+  }
   return SF_OK;
 }
 
 template <int KS, int NW, int TPW>
-int launch_eval_lds(sf_ctx* ctx, const double* coef, int64_t S,
+int launch_eval_lds(sf_ctx* ctx, const double* coef, int64_t S_all,
                            float* out, int64_t ring, unsigned flags,
                            unsigned* sums) {
   const int64_t P = ctx->n_pix;
   const int64_t run = EvalLds<NW, TPW>::kRun;
   const int64_t n_pb = (P + run - 1) / run;
-  const int groups = eval_chunk_groups(n_pb, S, ctx->eval_groups ? ctx->eval_groups : 16, 1024);
+  // 2 groups (32 slots) per item on small grids -- those whose pixel blocks
+  // are dealt to the XCDs interleaved (n_pb <= 64: 256^2 and below) -- else
+  // 16 (profiles/round2l_eval_chunks.txt: 256^2 x D = 20 in the bench,
+  // 0.72 -> 0.79 of 8 TB/s; 1 or 16 groups both lose)
+  const int def_groups = n_pb <= 64 ? 2 : 16;
+  const int groups = eval_chunk_groups(n_pb, S_all,
+                                       ctx->eval_groups ? ctx->eval_groups : def_groups, 1024);
+  const int64_t per = eval_launch_slots(ctx, n_pb, groups, 64 * NW);
+  for (int64_t b = 0; b < S_all; b += per) {
+  const int64_t S = S_all - b < per ? S_all - b : per;
   const int64_t n_sc = (S + 16 * groups - 1) / (16 * groups);
   const int64_t nblk = eval_grid(ctx, n_pb, n_sc, 64 * NW);
+  const double* cb = coef + b * ctx->D;
+  unsigned* sb = sums ? sums + b : nullptr;
   // auto XCD map: interleave the pixel blocks over the XCDs when each XCD's
   // contiguous eighth would be <= 8 blocks (measured: 256^2 at 4 KiB runs
   // +2-3 %, 512^2 -3 %; profiles/round1e_eval_xcd_map.txt)
+  unsigned fl = flags;
   if (ctx->eval_xcd_map < 0 && (n_pb & 7) == 0 && n_pb / 8 <= 8)
-    flags |= kEvalXcdInterleave;
+    fl |= kEvalXcdInterleave;
   if (flags & SF_EVAL_NT_STORES)
     hipLaunchKernelGGL((kl_eval_lds_kernel<KS, NW, TPW, true>), dim3((unsigned)nblk),
-                       dim3(64 * NW), 0, ctx->stream, ctx->d_cfrag, coef, ctx->D,
-                       ctx->ksteps, S, P, n_pb, n_sc, groups, out, ring, flags,
-                       ctx->eval_sleep, sums);
+                       dim3(64 * NW), 0, ctx->stream, ctx->d_cfrag, cb, ctx->D,
+                       ctx->ksteps, S, P, n_pb, n_sc, groups, out, ring, b % ring,
+                       fl, ctx->eval_sleep, sb);
   else
     hipLaunchKernelGGL((kl_eval_lds_kernel<KS, NW, TPW, false>), dim3((unsigned)nblk),
-                       dim3(64 * NW), 0, ctx->stream, ctx->d_cfrag, coef, ctx->D,
-                       ctx->ksteps, S, P, n_pb, n_sc, groups, out, ring, flags,
-                       ctx->eval_sleep, sums);
+                       dim3(64 * NW), 0, ctx->stream, ctx->d_cfrag, cb, ctx->D,
+                       ctx->ksteps, S, P, n_pb, n_sc, groups, out, ring, b % ring,
+                       fl, ctx->eval_sleep, sb);
   SF_HIP(hipGetLastError());
+  }
   return SF_OK;
 }
 
