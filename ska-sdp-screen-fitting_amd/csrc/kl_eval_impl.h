@@ -666,11 +666,15 @@ int launch_eval_lds(sf_ctx* ctx, const double* coef, int64_t S_all,
   const int64_t P = ctx->n_pix;
   const int64_t run = EvalLds<NW, TPW>::kRun;
   const int64_t n_pb = (P + run - 1) / run;
-  // 2 groups (32 slots) per item on small grids -- those whose pixel blocks
-  // are dealt to the XCDs interleaved (n_pb <= 64: 256^2 and below) -- else
-  // 16 (profiles/round2l_eval_chunks.txt: 256^2 x D = 20 in the bench,
-  // 0.72 -> 0.79 of 8 TB/s; 1 or 16 groups both lose)
-  const int def_groups = n_pb <= 64 ? 2 : 16;
+  // Small grids (n_pb <= 64: 256^2 and below, pixel blocks dealt to the XCDs
+  // interleaved): the shortest items whose Cpix reload (8 x 4 KS bytes per
+  // pixel) stays <= ~1/3 of their output (16 x 16 g bytes per pixel):
+  // KS <= 2 -> 1 group, 3-5 -> 2, 6-11 -> 4, else 8.  Measured in the bench
+  // setting (profiles/round2l_eval_chunks.txt): 256^2 x D = 20 0.72 (16
+  // groups) -> 0.79 (2 groups) of 8 TB/s, 1 group 0.67; 128^2 x D = 7 0.61
+  // -> 0.75 (1 group).  Larger grids keep 16 (their Cpix outgrows L2 and the
+  // long items won at 512^2, round2k_eval_split.txt).
+  const int def_groups = n_pb > 64 ? 16 : KS <= 2 ? 1 : KS <= 5 ? 2 : KS <= 11 ? 4 : 8;
   const int groups = eval_chunk_groups(n_pb, S_all,
                                        ctx->eval_groups ? ctx->eval_groups : def_groups, 1024);
   const int64_t per = eval_launch_slots(ctx, n_pb, groups, 64 * NW);

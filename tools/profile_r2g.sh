@@ -3,7 +3,7 @@
 # default bench (config 4), its kernel trace, PMC traffic / MFMA / fp64-VALU
 # passes of config 4, the config-5 shard and the config-3 gain screens.
 set -e
-O=gpurun_out/r2g_prof
+O=${PROF_OUT:-gpurun_out/r2g_prof}
 mkdir -p $O/c4trace
 export TMPDIR=/tmp
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/gputests.log 2>&1
