@@ -69,10 +69,14 @@ def parse():
     ap.add_argument("--no-side-legs", action="store_true",
                     help="skip the untimed side measurements (fp64-sincos "
                          "eval, fit alone on the whole chip)")
-    ap.add_argument("--chunks", type=int, default=2,
+    ap.add_argument("--chunks", type=int, default=1,
                     help="time chunks per step: the fit of chunk c+1 runs on a "
-                         "second stream while chunk c is evaluated (1 = fit "
-                         "then eval, serialised)")
+                         "second stream while chunk c is evaluated; 1 "
+                         "(default) = fit then eval on the whole chip.  The "
+                         "fit is 3 %% (config 4) / 8 %% (config 5) of the eval "
+                         "and takes SIMD and CU time from it when overlapped: "
+                         "serial config 4 5.92 M slots/s vs 5.81 pipelined "
+                         "(profiles/round2t_schedule_ab.txt)")
     ap.add_argument("--reserve-cus", type=int, default=-1,
                     help="compute units the eval stream leaves to the fit "
                          "stream (pipelined mode); -1 (default): 16 when "

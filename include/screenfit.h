@@ -135,6 +135,14 @@ int sf_device_cus(sf_ctx* ctx, int* n_cu);
  * evaluation work item (each item loads its pixel block's basis once, so
  * longer items re-read less of it). */
 #define SF_OPT_EVAL_GROUPS 8
+/* SF_OPT_EVAL_BANDS = b (1..128, power of two; 0 = auto): the evaluation
+ * runs its work items band-major over b pixel bands (every slot chunk of the
+ * first 1/b of the pixel blocks, then the next ...), so each XCD's live slice
+ * of the pixel basis is 1/b of its share.  Auto: bands of 128 pixel blocks
+ * (with the interleaved XCD map) for the register-tile kernels on grids of
+ * >= 1024 blocks (512^2 and up), else 1.  Ignored where the pixel blocks of a
+ * band would not divide by 8.  Outputs are identical for every b. */
+#define SF_OPT_EVAL_BANDS 9
 #define SF_EVAL_KERNEL_AUTO 0
 #define SF_EVAL_KERNEL_TILE 1
 #define SF_EVAL_KERNEL_LDS4 2

@@ -184,6 +184,11 @@ int sf_set_option(sf_ctx* ctx, int option, int value) {
                  SF_EINVAL, "sf_set_option: groups must be 0 or a power of two <= 256");
       ctx->eval_groups = value;
       return SF_OK;
+    case SF_OPT_EVAL_BANDS:
+      SF_REQUIRE(value >= 0 && value <= 128 && (value & (value - 1)) == 0,
+                 SF_EINVAL, "sf_set_option: bands must be 0 or a power of two <= 128");
+      ctx->eval_bands = value;
+      return SF_OK;
     case SF_OPT_EVAL_MAX_BLOCKS:
       SF_REQUIRE(value >= 0, SF_EINVAL, "sf_set_option: negative block cap");
       ctx->eval_max_blocks = value;

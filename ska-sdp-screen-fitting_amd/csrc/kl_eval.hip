@@ -127,7 +127,7 @@ int launch_eval(sf_ctx* ctx, const double* coef, const double* cxx,
   const bool lds = v != SF_EVAL_KERNEL_TILE && v != SF_EVAL_KERNEL_TILE3 &&
                    v != SF_EVAL_KERNEL_SHB;
   int ks = ctx->ksteps + (lds ? ctx->eval_ks_pad : 0);
-  flags &= ~kEvalXcdInterleave;
+  flags &= ~(kEvalXcdInterleave | kEvalBandMask);
   if (ctx->eval_xcd_map > 0) flags |= kEvalXcdInterleave;
   if (ks > 15) ks = ctx->ksteps;
   switch (ks) {

@@ -84,10 +84,26 @@ __device__ __forceinline__ void load_coef(double (&af)[KS],
 // Internal flag bit (never set by callers: sf_kl_eval masks it): XCD x takes
 // the pixel blocks pb = x (mod 8) instead of a contiguous eighth.
 constexpr unsigned kEvalXcdInterleave = 1u << 30;
+// Internal flag bits 27-29: log2 of the pixel bands (SF_OPT_EVAL_BANDS).  With
+// B bands the work items run band-major -- every slot chunk of band 0's pixel
+// blocks, then band 1's, ... -- and the XCD map applies within a band, so an
+// XCD's live Cpix slice is 1/B of its share: at 512^2 it outgrows the 4 MiB L2
+// (D = 20: 5.2 MB, D = 50: 13.6 MB per XCD) unless banded.
+constexpr int kEvalBandShift = 27;
+constexpr unsigned kEvalBandMask = 7u << kEvalBandShift;
 
-__device__ __forceinline__ void eval_block(int64_t bb, int64_t n_pb,
+__device__ __forceinline__ void eval_block(int64_t bb, int64_t n_pb, int64_t n_sc,
                                            int64_t& pb, int64_t& sc,
                                            unsigned flags) {
+  const int lb = (flags & kEvalBandMask) >> kEvalBandShift;
+  int64_t band = 0;
+  if (lb) {
+    // the launcher sets bands only when n_pb / B divides by 8
+    n_pb >>= lb;
+    const int64_t per_band = n_pb * n_sc;
+    band = bb / per_band;
+    bb -= band * per_band;
+  }
   if ((n_pb & 7) == 0) {
     const int64_t per = n_pb >> 3;
     const int64_t x = bb & 7, i = bb >> 3;
@@ -97,6 +113,16 @@ __device__ __forceinline__ void eval_block(int64_t bb, int64_t n_pb,
     pb = bb % n_pb;
     sc = bb / n_pb;
   }
+  pb += band * n_pb;
+}
+
+// log2 of the pixel bands of a launch over n_pb blocks: SF_OPT_EVAL_BANDS,
+// else auto_bands, while each band's blocks still divide by 8
+inline unsigned eval_band_flags(const sf_ctx* ctx, int64_t n_pb, int auto_bands = 1) {
+  int b = ctx->eval_bands ? ctx->eval_bands : auto_bands, lb = 0;
+  while (b > 1 && ((n_pb % ((int64_t)8 * b)) != 0)) b >>= 1;
+  while ((1 << lb) < b) ++lb;
+  return (unsigned)lb << kEvalBandShift;
 }
 
 // Precise epilogue (no SF_EVAL_FAST_SINCOS): sin / cos(2 pi rev) in fp64 to
@@ -205,7 +231,7 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
   const int64_t n_blocks = n_pb * n_sc;
   for (int64_t bb = blockIdx.x; bb < n_blocks; bb += gridDim.x) {
     int64_t pb, sc;
-    eval_block(bb, n_pb, pb, sc, flags);
+    eval_block(bb, n_pb, n_sc, pb, sc, flags);
     if (sc >= n_sc) continue;  // uniform per workgroup
     const int64_t wpb = SHB ? pb : pb * kEvalWaves + w;
     const int64_t p0 = wpb * kWavePix + (int64_t)(l & 15) * kTiles;
@@ -233,6 +259,19 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
     const bool scrub = flags & SF_EVAL_NAN_SCRUB;
     const bool be = flags & SF_EVAL_BIG_ENDIAN;
     const int64_t slot_base = sc * (int64_t)chunk_groups * 16;
+    // checksums: the slot sums of 4 consecutive groups of this wave are
+    // parked one per lane (lane 16 k + 4 gq + r <- slot row 4 r + k of the
+    // gq-th group) and leave as ONE 64-lane atomic instead of 16 (atomics run
+    // at the memory side, one wave-instruction per ~50 ns per CU)
+    unsigned pend = 0u;
+    uint32_t pslot = ~0u;
+    int gq = 0;
+    auto flush_sums = [&]() {
+      if (pslot != ~0u) atomicAdd(sums + pslot, pend);
+      pend = 0u;
+      pslot = ~0u;
+      gq = 0;
+    };
     for (int g = SHB ? w : 0; g < chunk_groups; g += SHB ? kEvalWaves : 1) {
       const int64_t s0 = slot_base + (int64_t)g * 16;
       if (s0 >= S) break;
@@ -363,7 +402,10 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
         if (sums) {
           // the 16 lanes of this slot row (one DPP row) hold its 64 pixels
           cs = row_sum16(cs);
-          if ((l & 15) == 0) atomicAdd(sums + s, cs);
+          if ((l & 15) == 4 * gq + r) {
+            pend = cs;
+            pslot = (uint32_t)s;
+          }
         }
       };
       if (be) {
@@ -373,7 +415,9 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
 #pragma unroll
         for (int r = 0; r < 4; ++r) row_out(r, std::false_type{});
       }
+      if (sums && ++gq == 4) flush_sums();
     }
+    if (sums) flush_sums();
   }  // workgroup walk
 }
 
@@ -409,13 +453,19 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
     int sleep, unsigned* __restrict__ sums) {
   using L = EvalLds<NW, TPW>;
   __shared__ float tile[2][16][L::kStride];
+  // checksums: slot sums of up to 16 groups per half ([half][group % 16]
+  // [row]); wave 0 adds a half's 256 consecutive slots with 4 64-lane
+  // atomics once the next half has begun, instead of one atomic per (wave,
+  // slot) -- atomics run at the memory side, one wave-instruction per ~50 ns
+  // per CU
+  __shared__ unsigned csum[2][16][16];
   const int l = threadIdx.x & 63;
   // wave index, wave-uniform: keeps slot / ring arithmetic on the SALU
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t n_blocks = n_pb * n_sc;
   for (int64_t bb = blockIdx.x; bb < n_blocks; bb += gridDim.x) {
     int64_t pb, sc;
-    eval_block(bb, n_pb, pb, sc, flags);
+    eval_block(bb, n_pb, n_sc, pb, sc, flags);
     if (sc >= n_sc) continue;  // uniform per workgroup
     const int wblk = w / L::kWavesPerBlock;         // 64-pixel block in the run
     const int t0 = (w % L::kWavesPerBlock) * TPW;   // first tile of this wave
@@ -435,9 +485,19 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
     const bool be = flags & SF_EVAL_BIG_ENDIAN;
     const int64_t pix0 = pb * L::kRun;
     const int64_t slot_base = sc * (int64_t)chunk_groups * 16;
+    // wave 0: add the csum entries of groups [g0, g0 + ng) (one half)
+    auto flush_sums = [&](int g0, int ng) {
+      const unsigned(*cs)[16] = csum[(g0 >> 4) & 1];
+      for (int i = l; i < ng * 16; i += 64) {
+        const int64_t s = slot_base + (int64_t)g0 * 16 + i;
+        if (s < S) atomicAdd(sums + s, cs[i >> 4][i & 15]);
+      }
+    };
+    int ng_done = 0;
     for (int g = 0; g < chunk_groups; ++g) {
       const int64_t s0 = slot_base + (int64_t)g * 16;
       if (s0 >= S) break;  // uniform per workgroup
+      ng_done = g + 1;
       float(*buf)[L::kStride] = tile[g & 1];
       // ---- contraction: 16 slots x this wave's 64 pixels
       double af[KS];
@@ -464,6 +524,8 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
       }
       for (int z = 0; z < sleep; ++z) __builtin_amdgcn_s_sleep(1);
       __syncthreads();
+      // every wave wrote its sums of groups < g before this barrier
+      if (sums && w == 0 && g >= 16 && (g & 15) == 0) flush_sums(g - 16, 16);
       // ---- stores: wave w owns kSlotsPerWave slots of the group
       // BE (FITS byte order) as a compile-time branch of a whole slot
       auto slot_out = [&](int j, auto be_tag) {
@@ -515,7 +577,7 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
                                (unsigned)__builtin_amdgcn_readlane((int)cs, 16) +
                                (unsigned)__builtin_amdgcn_readlane((int)cs, 32) +
                                (unsigned)__builtin_amdgcn_readlane((int)cs, 48);
-          if (l == 0) atomicAdd(sums + s, tot);
+          if (l == 0) csum[(g >> 4) & 1][g & 15][row] = tot;
         }
       };
       if (be) {
@@ -528,6 +590,14 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
     }
     // the next workgroup item reuses the LDS tiles from buffer 0
     __syncthreads();
+    if (sums) {
+      // the last (partial) half: every wave's sums are in after the barrier
+      if (w == 0 && ng_done > 0) {
+        const int g0 = ((ng_done - 1) >> 4) << 4;
+        flush_sums(g0, ng_done - g0);
+      }
+      __syncthreads();  // before a next item's waves write csum again
+    }
   }  // workgroup walk
 }
 
@@ -586,6 +656,14 @@ int launch_eval_ks(sf_ctx* ctx, const double* coef,
   const int64_t n_pb = ctx->n_pix_blocks;
   const int groups = eval_chunk_groups(n_pb, S_all, ctx->eval_groups ? ctx->eval_groups : 64, 2048);
   const int64_t per = eval_launch_slots(ctx, n_pb, groups, 256);
+  // large grids (>= 1024 blocks of 256 px: 512^2 and up): auto bands of 128
+  // blocks with the XCD-interleaved map -- 512^2 x D = 50 0.706 -> 0.732 of
+  // 8 TB/s; 2, 4 or 16 bands and the contiguous map measured no better
+  // (profiles/round2u_eval_bands.txt)
+  const int auto_bands = n_pb >= 1024 ? (int)(n_pb / 128 < 128 ? n_pb / 128 : 128) : 1;
+  unsigned fl = flags | eval_band_flags(ctx, n_pb, auto_bands);
+  if (ctx->eval_xcd_map < 0 && ctx->eval_bands == 0 && auto_bands > 1)
+    fl |= kEvalXcdInterleave;
   for (int64_t b = 0; b < S_all; b += per) {
   const int64_t S = S_all - b < per ? S_all - b : per;
   const int64_t n_sc = (S + 16 * groups - 1) / (16 * groups);
@@ -601,7 +679,7 @@ int launch_eval_ks(sf_ctx* ctx, const double* coef,
 #define SF_LAUNCH(V, F, N, G)                                                 \
   hipLaunchKernelGGL((kl_eval_kernel<KS, MINW, V, F, N, G>), dim3((unsigned)nblk),  \
                      dim3(256), 0, ctx->stream, ctx->d_cfrag, cb, cxb, cyb, \
-                     ctx->D, S, P, n_pb, n_sc, groups, out, ring, b % ring, flags, sb)
+                     ctx->D, S, P, n_pb, n_sc, groups, out, ring, b % ring, fl, sb)
 #define SF_LAUNCH_G(V, F, N) \
   do {                       \
     if (gain)                \
@@ -647,7 +725,8 @@ int launch_eval_shb(sf_ctx* ctx, const double* coef, int64_t S_all,
   hipLaunchKernelGGL((kl_eval_kernel<KS, 4, true, F, N, false, true>),          \
                      dim3((unsigned)nblk), dim3(256), 0, ctx->stream,           \
                      ctx->d_cfrag, cb, nullptr, nullptr, ctx->D, S, P, n_wpb, \
-                     n_sc, groups, out, ring, b % ring, flags, sb)
+                     n_sc, groups, out, ring, b % ring,                         \
+                     flags | eval_band_flags(ctx, n_wpb), sb)
   if (fast) {
     if (nt) SF_LAUNCH_SHB(true, true); else SF_LAUNCH_SHB(true, false);
   } else {
@@ -690,6 +769,7 @@ int launch_eval_lds(sf_ctx* ctx, const double* coef, int64_t S_all,
   unsigned fl = flags;
   if (ctx->eval_xcd_map < 0 && (n_pb & 7) == 0 && n_pb / 8 <= 8)
     fl |= kEvalXcdInterleave;
+  fl |= eval_band_flags(ctx, n_pb);
   if (flags & SF_EVAL_NT_STORES)
     hipLaunchKernelGGL((kl_eval_lds_kernel<KS, NW, TPW, true>), dim3((unsigned)nblk),
                        dim3(64 * NW), 0, ctx->stream, ctx->d_cfrag, cb, ctx->D,

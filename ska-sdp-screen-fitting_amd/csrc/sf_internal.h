@@ -93,6 +93,7 @@ struct sf_ctx {
   int eval_sleep = 0;           // SF_OPT_EVAL_SLEEP: x 64 cycles per group
   int eval_xcd_map = -1;        // SF_OPT_EVAL_XCD_MAP (-1 = auto)
   int eval_groups = 0;          // SF_OPT_EVAL_GROUPS (0 = auto = 256)
+  int eval_bands = 0;           // SF_OPT_EVAL_BANDS (0 = auto = 1)
   int fit_pack = 1;             // SF_OPT_FIT_PACK: 2 slots per wave for D <= 32
 };
 

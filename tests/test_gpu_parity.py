@@ -433,8 +433,8 @@ def test_eval_kernels_agree(ctx, dev, n_dir, grid):
     from ska_sdp_screen_fitting_amd._lib import (
         EVAL_KERNEL_NAMES, SF_EVAL_BIG_ENDIAN, SF_EVAL_FAST_SINCOS,
         SF_EVAL_KERNEL_AUTO, SF_EVAL_KERNEL_TILE, SF_EVAL_NT_STORES,
-        SF_OPT_EVAL_KERNEL, SF_OPT_EVAL_KS_PAD, SF_OPT_EVAL_MAX_BLOCKS,
-        SF_OPT_EVAL_XCD_MAP)
+        SF_OPT_EVAL_BANDS, SF_OPT_EVAL_KERNEL, SF_OPT_EVAL_KS_PAD,
+        SF_OPT_EVAL_MAX_BLOCKS, SF_OPT_EVAL_XCD_MAP)
     from ska_sdp_screen_fitting_amd.synthetic import make_solutions
     s = make_solutions(n_ant=2, n_time=2, n_freq=1, n_dir=n_dir, seed=4)
     pp, mra, mdec = geometry.piercepoints(s.dir_radec)
@@ -466,6 +466,11 @@ def test_eval_kernels_agree(ctx, dev, n_dir, grid):
                 ctx.set_option(SF_OPT_EVAL_XCD_MAP, xm)
                 outs[(kv, "xcd", xm)] = gpu_eval(ctx, dev, pp, x, y, coef, flags=base)
             ctx.set_option(SF_OPT_EVAL_XCD_MAP, -1)
+            # band-major work-item order over 2 / 4 pixel bands
+            for nb in (2, 4):
+                ctx.set_option(SF_OPT_EVAL_BANDS, nb)
+                outs[(kv, "bands", nb)] = gpu_eval(ctx, dev, pp, x, y, coef, flags=base)
+            ctx.set_option(SF_OPT_EVAL_BANDS, 0)
             # zero k-step padding of the contraction
             ctx.set_option(SF_OPT_EVAL_KS_PAD, 2)
             outs[(kv, "pad")] = gpu_eval(ctx, dev, pp, x, y, coef, flags=base)
@@ -480,6 +485,7 @@ def test_eval_kernels_agree(ctx, dev, n_dir, grid):
         ctx.set_option(SF_OPT_EVAL_MAX_BLOCKS, 0)
         ctx.set_option(SF_OPT_EVAL_XCD_MAP, -1)
         ctx.set_option(SF_OPT_EVAL_KS_PAD, 0)
+        ctx.set_option(SF_OPT_EVAL_BANDS, 0)
     ref = outs[(SF_EVAL_KERNEL_TILE, 0)]
     for k, o in outs.items():
         if k[1] == "noscrub":
@@ -494,6 +500,51 @@ def test_eval_kernels_agree(ctx, dev, n_dir, grid):
     good = np.isfinite(coef).all(axis=1)
     want = okl.eval_planes(okl.eval_phase_screens(coef[good], cpix))
     np.testing.assert_allclose(ref[good].reshape(want.shape), want, rtol=0, atol=2e-6)
+
+
+def test_eval_bands_512(ctx, dev):
+    """512^2 x D = 50 (config 5's grid): the auto pixel bands of the register
+    tile (8 bands of 128 blocks, interleaved XCD map), explicit 1 / 2 / 16
+    bands and both maps, and the auto kernel write the same bits as the
+    unbanded contiguous launch; sampled slots match the oracle."""
+    from ska_sdp_screen_fitting_amd import geometry
+    from ska_sdp_screen_fitting_amd._lib import (
+        SF_EVAL_FAST_SINCOS, SF_EVAL_KERNEL_AUTO, SF_EVAL_KERNEL_TILE,
+        SF_OPT_EVAL_BANDS, SF_OPT_EVAL_KERNEL, SF_OPT_EVAL_XCD_MAP)
+    from ska_sdp_screen_fitting_amd.synthetic import make_solutions
+    n_dir, grid = 50, 512
+    s = make_solutions(n_ant=2, n_time=2, n_freq=1, n_dir=n_dir, seed=5)
+    pp, mra, mdec = geometry.piercepoints(s.dir_radec)
+    cell = FIELD["width"] / (grid - 0.5)
+    x, y = geometry.grid_coords(FIELD["rad"], FIELD["dec"], FIELD["width"],
+                                cell, mra, mdec)
+    rng = np.random.default_rng(512)
+    coef = rng.normal(0, 0.01, size=(37, n_dir))
+    coef[7, 3] = np.nan
+    base = 1 | SF_EVAL_FAST_SINCOS
+    try:
+        ctx.set_option(SF_OPT_EVAL_KERNEL, SF_EVAL_KERNEL_TILE)
+        ctx.set_option(SF_OPT_EVAL_XCD_MAP, 0)
+        ctx.set_option(SF_OPT_EVAL_BANDS, 1)
+        ref = gpu_eval(ctx, dev, pp, x, y, coef, flags=base)
+        for kv, xm, nb in ((SF_EVAL_KERNEL_TILE, -1, 0), (SF_EVAL_KERNEL_TILE, 1, 2),
+                           (SF_EVAL_KERNEL_TILE, 0, 16), (SF_EVAL_KERNEL_TILE, 1, 128),
+                           (SF_EVAL_KERNEL_AUTO, -1, 0), (SF_EVAL_KERNEL_AUTO, -1, 4)):
+            ctx.set_option(SF_OPT_EVAL_KERNEL, kv)
+            ctx.set_option(SF_OPT_EVAL_XCD_MAP, xm)
+            ctx.set_option(SF_OPT_EVAL_BANDS, nb)
+            o = gpu_eval(ctx, dev, pp, x, y, coef, flags=base)
+            assert np.array_equal(o.view(np.int32), ref.view(np.int32)), (kv, xm, nb)
+            del o
+    finally:
+        ctx.set_option(SF_OPT_EVAL_KERNEL, SF_EVAL_KERNEL_AUTO)
+        ctx.set_option(SF_OPT_EVAL_XCD_MAP, -1)
+        ctx.set_option(SF_OPT_EVAL_BANDS, 0)
+    assert np.all(ref[7, 0::2] == 1.0) and np.all(ref[7, 1::2] == 0.0)
+    cpix = okl.cpix_matrix(pp, x, y)
+    pick = [0, 8, 36]
+    want = okl.eval_planes(okl.eval_phase_screens(coef[pick], cpix))
+    np.testing.assert_allclose(ref[pick].reshape(want.shape), want, rtol=0, atol=2e-6)
 
 
 def test_binding_rejects_bad_device_operands(ctx, dev):

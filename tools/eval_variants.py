@@ -22,7 +22,7 @@ from ska_sdp_screen_fitting_amd._lib import (  # noqa: E402
     SF_EVAL_KERNEL_LDS16H, SF_EVAL_KERNEL_SHB, SF_EVAL_KERNEL_TILE, SF_EVAL_KERNEL_TILE3,
     SF_EVAL_NAN_SCRUB, SF_EVAL_NT_STORES, SF_OPT_EVAL_KERNEL,
     SF_OPT_EVAL_GROUPS, SF_OPT_EVAL_KS_PAD, SF_OPT_EVAL_SLEEP,
-    SF_OPT_EVAL_XCD_MAP)
+    SF_OPT_EVAL_XCD_MAP, SF_OPT_EVAL_BANDS)
 
 KERNELS = {"auto": SF_EVAL_KERNEL_AUTO, "tile": SF_EVAL_KERNEL_TILE,
            "tile3": SF_EVAL_KERNEL_TILE3,
@@ -46,9 +46,10 @@ ctx.set_stream(stream.cuda_stream)
 base = SF_EVAL_NAN_SCRUB | SF_EVAL_FAST_SINCOS
 variants = {}
 for v in args.variants.split(","):
-    # kernel[+nt][+padN][+sleepN][+xi][+gN]
+    # kernel[+nt][+padN][+sleepN][+xi|+xc][+gN][+bN]; the XCD map is the
+    # library's auto choice unless +xi (interleaved) / +xc (contiguous)
     k, *mods = v.split("+")
-    fl, pad, sleep, xi, grp = base, 0, 0, 0, 0
+    fl, pad, sleep, xi, grp, bands = base, 0, 0, -1, 0, 0
     for m in mods:
         if m == "nt":
             fl |= SF_EVAL_NT_STORES
@@ -58,15 +59,20 @@ for v in args.variants.split(","):
             sleep = int(m[5:])
         elif m == "xi":
             xi = 1
+        elif m == "xc":
+            xi = 0
+        elif m.startswith("b"):
+            bands = int(m[1:])
         elif m.startswith("g"):
             grp = int(m[1:])
         else:
             raise SystemExit(f"unknown variant modifier {m}")
-    variants[v] = (KERNELS[k], fl, (pad, sleep, xi, grp))
+    variants[v] = (KERNELS[k], fl, (pad, sleep, xi, grp, bands))
 
 
-def use(kv, opts=(0, 0, 0, 0)):
-    pad, sleep, xi, grp = opts
+def use(kv, opts=(0, 0, -1, 0, 0)):
+    pad, sleep, xi, grp, bands = opts
+    ctx.set_option(SF_OPT_EVAL_BANDS, bands)
     ctx.set_option(SF_OPT_EVAL_GROUPS, grp)
     ctx.set_option(SF_OPT_EVAL_KERNEL, kv)
     ctx.set_option(SF_OPT_EVAL_KS_PAD, pad)

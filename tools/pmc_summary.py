@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Per-launch PMC figures of one kernel from the CSVs of tools/pmc_passes.sh:
-counters averaged over the kernel's full-grid launches (small launches --
-cross-checks, single-slot checks -- dropped), plus derived fractions:
+"""Per-call PMC figures of one kernel from the CSVs of tools/pmc_passes.sh:
+counters summed over the dispatches of one call and averaged over the calls
+(small launches -- cross-checks, single-slot checks -- dropped), plus derived
+fractions:
 
 * mfma_busy_frac  = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x CUs x 4)
   (GRBM_GUI_ACTIVE sums the 8 XCDs; MFMA busy cycles sum the SIMDs)
@@ -33,7 +34,8 @@ def load(d, kernel):
             per[key][r["Counter_Name"]] += float(r["Counter_Value"])
             meta[key] = (int(r["Grid_Size"]), r["Kernel_Name"].split("(")[0],
                          int(r["End_Timestamp"]) - int(r["Start_Timestamp"]),
-                         r.get("VGPR_Count"), r.get("LDS_Block_Size"))
+                         r.get("VGPR_Count"), r.get("LDS_Block_Size"),
+                         int(r["Start_Timestamp"]))
     return per, meta
 
 
@@ -44,23 +46,50 @@ def main():
                     help="substring of the full kernel name (template args included)")
     ap.add_argument("--cus", type=int, default=256)
     ap.add_argument("--json", action="store_true")
+    ap.add_argument("--group", type=int, default=0,
+                    help="dispatches per call (default: a call ends at a "
+                    "partial-grid dispatch)")
     a = ap.parse_args()
     per, meta = load(a.dir, a.kernel)
     if not per:
         raise SystemExit(f"no {a.kernel} dispatches under {a.dir}")
     big = max(m[0] for m in meta.values())
-    keys = [k for k in per if meta[k][0] == big]
-    # average every counter over the full-grid dispatches that collected it
+    # bulk dispatches (cross-check launches of a few slots dropped), grouped
+    # into calls: sf_kl_eval splits a call longer than 2^31 work-items into
+    # one-shot dispatches, so within each pass file a call is the run of
+    # consecutive bulk dispatches ending at a partial-grid one (or --group N
+    # dispatches each); counters and durations are summed per call
+    groups = []
+    for path in sorted({k[0] for k in per}):
+        ks = sorted((k for k in per if k[0] == path and meta[k][0] * 64 >= big),
+                    key=lambda k: meta[k][5])
+        cur = []
+        for k in ks:
+            cur.append(k)
+            if (a.group and len(cur) == a.group) or (not a.group and meta[k][0] < big) \
+                    or (not a.group and len({meta[x][0] for x in ks}) == 1):
+                groups.append(cur)
+                cur = []
+        if cur:
+            groups.append(cur)
+    # average every counter over the calls that collected it
     sums, cnt = defaultdict(float), defaultdict(int)
-    for k in keys:
-        for c, v in per[k].items():
+    for g in groups:
+        tot = defaultdict(float)
+        for k in g:
+            for c, v in per[k].items():
+                tot[c] += v
+        for c, v in tot.items():
             sums[c] += v
             cnt[c] += 1
     avg = {c: sums[c] / cnt[c] for c in sums}
-    dur = sum(meta[k][2] for k in keys) / len(keys) * 1e-6
-    res = {"kernel": meta[keys[0]][1], "grid": big, "dispatches": len(keys),
-           "avg_ms_under_pmc": dur, "vgpr": meta[keys[0]][3],
-           "lds_bytes": meta[keys[0]][4], "counters": avg}
+    dur = sum(meta[k][2] for g in groups for k in g) / len(groups) * 1e-6
+    k0 = groups[0][0]
+    res = {"kernel": meta[k0][1], "grid": big, "dispatches": len(groups),
+           "dispatches_per_call": [len(g) for g in groups],
+           "work_items_per_call": sum(meta[k][0] for k in groups[0]),
+           "avg_ms_under_pmc": dur, "vgpr": meta[k0][3],
+           "lds_bytes": meta[k0][4], "counters": avg}
     g = avg.get("GRBM_GUI_ACTIVE")
     simd_cyc = g / 8 * a.cus * 4 if g else None
     d = {}

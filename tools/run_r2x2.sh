@@ -1,0 +1,12 @@
+#!/bin/bash
+# Checksum-atomic batching: GPU tests, then config 4 / config 5 benches with
+# the side legs (eval without checksums) for the checksum cost
+set -e
+O=gpurun_out/r2x2
+mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/gputests.log 2>&1
+echo tests done
+timeout -k 10 300 python3 -u bench.py --no-cpu-baseline --no-fits --steps 10 > $O/c4.json 2> $O/c4.err
+echo c4 done
+timeout -k 10 400 python3 -u bench.py --workload config5 --no-cpu-baseline --no-fits --steps 2 --warmup 1 > $O/c5.json 2> $O/c5.err
+echo ALL DONE
