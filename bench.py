@@ -635,8 +635,13 @@ def main():
         traffic = None
         wkey = args.workload + ("-gain" if gain else "")
         tj = _profile_entry("traffic.json", wkey, eval_kernel_name)
+        # the PMC table's figure counts only when it was taken on this very
+        # call shape (same flags, chunks and algorithmic bytes per call: a
+        # sharded run's calls are smaller than the N = 1 run it was measured on)
         if (tj is not None and tj.get("flags") == flags
-                and tj.get("chunks", 1) == n_chunks):
+                and tj.get("chunks", 1) == n_chunks
+                and abs(tj.get("algorithmic_bytes_per_launch", 0) - launch_bytes)
+                <= 1e-6 * launch_bytes):
             traffic = tj.get("hbm_bytes_per_launch")
         ceil = side.get("store_ceiling") if side else None
         line = {
