@@ -143,6 +143,12 @@ int sf_device_cus(sf_ctx* ctx, int* n_cu);
  * >= 1024 blocks (512^2 and up), else 1.  Ignored where the pixel blocks of a
  * band would not divide by 8.  Outputs are identical for every b. */
 #define SF_OPT_EVAL_BANDS 9
+/* SF_OPT_FIT_LEAN = 0 / 1 (default 1): when every slot's unflagged weights
+ * are equal (counted by the classify kernel), the fit passes run a variant
+ * with no per-slot normal-matrix / subset-basis copies in LDS (flagged slots
+ * read their subset basis from the pool), for 2.7-4x the resident waves.
+ * Same results bit for bit; 0 forces the general layout. */
+#define SF_OPT_FIT_LEAN 10
 #define SF_EVAL_KERNEL_AUTO 0
 #define SF_EVAL_KERNEL_TILE 1
 #define SF_EVAL_KERNEL_LDS4 2

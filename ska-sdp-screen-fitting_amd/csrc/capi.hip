@@ -164,6 +164,9 @@ int sf_set_option(sf_ctx* ctx, int option, int value) {
     case SF_OPT_FIT_PACK:
       ctx->fit_pack = value != 0;
       return SF_OK;
+    case SF_OPT_FIT_LEAN:
+      ctx->fit_lean = value != 0;
+      return SF_OK;
     case SF_OPT_EVAL_KS_PAD:
       SF_REQUIRE(value >= 0 && value <= 3, SF_EINVAL,
                  "sf_set_option: k-step padding must be 0..3");

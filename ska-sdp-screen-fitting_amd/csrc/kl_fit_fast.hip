@@ -107,6 +107,12 @@ __global__ __launch_bounds__(256) void kl_classify_kernel(
   const unsigned long long gmask = (GW == 64) ? ~0ull : ((1ull << GW) - 1ull);
   const unsigned long long mask = (bm >> (g * GW)) & gmask;
   const bool tiny = ((bt >> (g * GW)) & gmask) != 0ull;
+  // unequal positive weights in the slot (U_k^T W U_k != w I): compared with
+  // the group's first unflagged weight; zeroing weights (outlier flags) keeps
+  // a uniform slot uniform, so one count per fit decides the pass kernel
+  const float w_first = __shfl(x, g * GW + (mask ? __builtin_ctzll(mask) : 0));
+  const unsigned long long bn = __ballot(live && x > 0.0f && x != w_first);
+  const bool nonuniform = ((bn >> (g * GW)) & gmask) != 0ull;
   if (d != 0 || s >= S) return;
   const int a = (int)(s % A);
   const int f = (int)((s / A) % F);
@@ -118,6 +124,7 @@ __global__ __launch_bounds__(256) void kl_classify_kernel(
   }
   order_out[s] = st_order[a];
   if (tiny) atomicAdd(counters + 2, 1);
+  else if (nonuniform) atomicAdd(counters + 4, 1);
   cls[s] = tiny ? 2 : 0;
   const unsigned long long full = (D == 64) ? ~0ull : ((1ull << D) - 1ull);
   if (mask == full) pos[s] = -1;
@@ -206,7 +213,8 @@ struct FastLds {
 __host__ __device__ inline size_t fast_shared_bytes(int D) {
   return (size_t)(2 * D * ldo(D) + 64) * sizeof(double);
 }
-__host__ __device__ inline size_t fast_wave_bytes(int D, bool slow) {
+__host__ __device__ inline size_t fast_wave_bytes(int D, bool slow, bool lean = false) {
+  if (lean) return (size_t)6 * 64 * sizeof(double);  // the vectors only
   return (size_t)((slow ? 3 : 2) * D * ldo(D) + 64 + 6 * 64) * sizeof(double) +
          (slow ? 64 * sizeof(double2) + 96 * sizeof(int2) : 0);
 }
@@ -214,7 +222,8 @@ __host__ __device__ inline size_t fast_wave_bytes(int D, bool slow) {
 struct Basis {
   int n;
   bool full;
-  const double* U;
+  int ld;             // row stride of U
+  const double* U;    // LDS (full basis, or a copied subset) or the global pool
   const double* lam;
 };
 
@@ -226,7 +235,7 @@ __device__ __forceinline__ double model_value(int screen_type, double x) {
 // One _fit_screen (stationscreen.py:433-594) in the eigenbasis.  Lanes p < n
 // carry the unflagged directions (phi_p, w_p); returns, per DIRECTION lane d,
 // white_d and resid_d.
-template <bool SLOW, int SPW>
+template <bool SLOW, int SPW, bool LEAN>
 __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
                          int K, int screen_type, bool uniform, double wu,
                          double phi_p, double w_p, double phi_d, double w_d,
@@ -259,13 +268,13 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
   double a1 = 0.0, a2 = 0.0;
   if (l < K) {
     for (int p = 0; p < n; ++p) {
-      const double u = B.U[p * ld + l];
+      const double u = B.U[p * B.ld + l];
       a1 += u * v0[p];
       a2 += u * v1[p];
     }
   }
   if (K > 0) {
-    if (!SLOW && uniform) {
+    if (!SLOW && (LEAN || uniform)) {
       // U_k^T (w I) U_k = w I  (U_k orthonormal over the unflagged rows)
       a1 /= wu;
       a2 /= wu;
@@ -274,7 +283,7 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
         for (int j = 0; j < K; ++j) {
           double s = 0.0;
           for (int p = 0; p < n; ++p)
-            s += B.U[p * ld + l] * (v2[p] * B.U[p * ld + j]);
+            s += B.U[p * B.ld + l] * (v2[p] * B.U[p * B.ld + j]);
           L.G[l * ld + j] = s;
         }
       }
@@ -330,7 +339,7 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
   if (l < n) {
     double cre = 0.0, cim = 0.0;
     for (int k = 0; k < K; ++k) {
-      const double u = B.U[l * ld + k];
+      const double u = B.U[l * B.ld + k];
       cre += u * v0[k];
       cim += u * v1[k];
     }
@@ -342,7 +351,7 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
   // s_hat = U^T screen; white = U Lambda^+ s_hat; C white = U (Lambda Lambda^+) s_hat
   if (l < n) {
     double sh = 0.0;
-    for (int p = 0; p < n; ++p) sh += B.U[p * ld + l] * v2[p];
+    for (int p = 0; p < n; ++p) sh += B.U[p * B.ld + l] * v2[p];
     const double lm = B.lam[l];
     const bool keep = fabs(lm) > kAtol;
     v0[l] = keep ? sh / lm : 0.0;
@@ -352,7 +361,7 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
   double white = 0.0, cw = 0.0;
   if (l < n) {
     for (int r = 0; r < n; ++r) {
-      const double u = B.U[l * ld + r];
+      const double u = B.U[l * B.ld + r];
       white += u * v0[r];
       cw += u * v1[r];
     }
@@ -416,8 +425,16 @@ __device__ __forceinline__ double screen_diff(int screen_type, double val,
   return resid;
 }
 
-template <bool SLOW, int SPW>
-__global__ __launch_bounds__(256) void kl_fit_pass_kernel(
+// LEAN (fast class, every slot's unflagged weights equal -- the 0/1 weights
+// of the benchmarks): no per-slot G / subset-basis copies in LDS -- a flagged
+// slot reads its subset basis straight from the pool (L1/L2) -- so the
+// per-slot LDS is the 3 KiB of vectors and 2.7x (D = 20) to 4x (D = 50) more
+// waves fit on a CU; the kernel is latency-bound, so occupancy is its speed.
+#ifndef SF_FIT_MINW
+#define SF_FIT_MINW 1  // waves per SIMD the register budget must admit
+#endif
+template <bool SLOW, int SPW, bool LEAN>
+__global__ __launch_bounds__(256, SF_FIT_MINW) void kl_fit_pass_kernel(
     int it, int niter, int64_t S, int F, int A, int D,
     const double* __restrict__ phase, const double* __restrict__ refph,
     int ref_sub, const double* __restrict__ g_u, const double* __restrict__ g_c,
@@ -450,14 +467,21 @@ __global__ __launch_bounds__(256) void kl_fit_pass_kernel(
   L.U = sU;
   L.C = sC;
   L.lam = sl;
-  double* wb = sl + 64 + (size_t)wv * (fast_wave_bytes(D, SLOW) / sizeof(double));
-  L.Vs = wb;
-  L.G = wb + D * ld;
-  L.M = L.G + D * ld;
-  L.lams = (SLOW ? L.M + D * ld : L.G + D * ld);
-  L.vec = L.lams + 64;
-  L.cs = reinterpret_cast<double2*>(L.vec + 6 * 64);
-  L.pr = reinterpret_cast<int2*>(L.cs + 64);
+  double* wb = sl + 64 + (size_t)wv * (fast_wave_bytes(D, SLOW, LEAN) / sizeof(double));
+  if (LEAN) {
+    L.Vs = L.G = L.M = L.lams = nullptr;
+    L.vec = wb;
+    L.cs = nullptr;
+    L.pr = nullptr;
+  } else {
+    L.Vs = wb;
+    L.G = wb + D * ld;
+    L.M = L.G + D * ld;
+    L.lams = (SLOW ? L.M + D * ld : L.G + D * ld);
+    L.vec = L.lams + 64;
+    L.cs = reinterpret_cast<double2*>(L.vec + 6 * 64);
+    L.pr = reinterpret_cast<int2*>(L.cs + 64);
+  }
   const uint8_t want = SLOW ? 2 : 0;
 
   for (int64_t s = (int64_t)blockIdx.x * nslots + wv; s < S;
@@ -493,17 +517,24 @@ __global__ __launch_bounds__(256) void kl_fit_pass_kernel(
     Basis B;
     B.n = n_unfl;
     B.full = (n_unfl == D);
+    B.ld = ld;
     if (B.full) {
       B.U = L.U;
       B.lam = L.lam;
     } else if (n_unfl > 0) {
       const double* e = pool + (size_t)id * (D * D + D);
-      for (int r = 0; r < n_unfl; ++r)
-        if (d < n_unfl) L.Vs[r * ld + d] = e[r * D + d];
-      if (d < n_unfl) L.lams[d] = e[D * D + d];
-      lds_sync();
-      B.U = L.Vs;
-      B.lam = L.lams;
+      if (LEAN) {
+        B.U = e;
+        B.ld = D;
+        B.lam = e + D * D;
+      } else {
+        for (int r = 0; r < n_unfl; ++r)
+          if (d < n_unfl) L.Vs[r * ld + d] = e[r * D + d];
+        if (d < n_unfl) L.lams[d] = e[D * D + d];
+        lds_sync();
+        B.U = L.Vs;
+        B.lam = L.lams;
+      }
     }
     // unflagged directions onto lanes p < n
     double phi_p = 0.0, w_p = 0.0;
@@ -525,11 +556,15 @@ __global__ __launch_bounds__(256) void kl_fit_pass_kernel(
     const double wmax = G::max(unfl ? w_d : -INFINITY);
     const double wmin = -G::max(unfl ? -w_d : -INFINITY);
     const bool uniform = (wmax == wmin);
+    if (LEAN && n_unfl > 0 && !uniform) {  // classify counted none: flag it loudly
+      if (d == 0) atomicOr(counters + 3, 4);
+      continue;
+    }
 
     if (n_unfl > 0) {
       if (order > n_unfl - 1) order = n_unfl - 1;
       if (it == 0) {
-        fit_once<SLOW, SPW>(L, B, D, ld, (int)order, screen_type, uniform, wmin,
+        fit_once<SLOW, SPW, LEAN>(L, B, D, ld, (int)order, screen_type, uniform, wmin,
                        phi_p, w_p, phi_d, w_d, white_d, resid_d);
       } else if (adjust_order) {
         bool hit_upper = false, hit_lower = false, hit_upper2 = false,
@@ -538,7 +573,7 @@ __global__ __launch_bounds__(256) void kl_fit_pass_kernel(
         for (int oi = 0; oi < 4; ++oi) {
           // oi == 0: the weights always compare equal (quirk Q2) -> no fit
           if (oi > 0)
-            fit_once<SLOW, SPW>(L, B, D, ld, (int)order, screen_type, uniform, wmin,
+            fit_once<SLOW, SPW, LEAN>(L, B, D, ld, (int)order, screen_type, uniform, wmin,
                            phi_p, w_p, phi_d, w_d, white_d, resid_d);
           if (hit_lower2 || hit_upper2) break;
           double redchi2;
@@ -757,7 +792,7 @@ __global__ __launch_bounds__(256) void kl_fill_mask_kernel(
 }
 
 // number new masks, make sure the pool holds them, decompose them
-static int number_and_decompose(sf_ctx* ctx, int* n_slow) {
+static int number_and_decompose(sf_ctx* ctx, int* n_slow, int* n_nonuniform) {
   SF_HIP(hipMemcpyAsync(ctx->d_counters + 1, ctx->d_counters, sizeof(int),
                         hipMemcpyDeviceToDevice, ctx->stream));
   const int cap = (int)ctx->table_cap;
@@ -766,11 +801,12 @@ static int number_and_decompose(sf_ctx* ctx, int* n_slow) {
                      ctx->stream, ctx->d_keys, cap, ctx->d_ids,
                      ctx->d_pool_mask, old_cap, ctx->d_counters);
   SF_HIP(hipGetLastError());
-  int cnt[3];
-  SF_HIP(hipMemcpyAsync(cnt, ctx->d_counters, 3 * sizeof(int),
+  int cnt[5];
+  SF_HIP(hipMemcpyAsync(cnt, ctx->d_counters, 5 * sizeof(int),
                         hipMemcpyDeviceToHost, ctx->stream));
   SF_HIP(hipStreamSynchronize(ctx->stream));
   *n_slow = cnt[2];
+  *n_nonuniform = cnt[4];
   if (cnt[0] > old_cap) {
     SF_TRYF(ensure_pool(ctx, (size_t)cnt[0]));
     hipLaunchKernelGGL(kl_fill_mask_kernel, dim3((cap + 255) / 256), dim3(256),
@@ -797,14 +833,14 @@ static int number_and_decompose(sf_ctx* ctx, int* n_slow) {
   return SF_OK;
 }
 
-template <bool SLOW, int SPW>
+template <bool SLOW, int SPW, bool LEAN>
 static int launch_pass_spw(sf_ctx* ctx, int it, const sf_fit_params* p,
                            const RefSpec& r, int64_t S, int F, int A,
                            const double* phase, double* coef, double* resid,
                            float* w_out, int32_t* order_out) {
   const int D = ctx->D;
   const size_t shared = fast_shared_bytes(D);
-  const size_t slot = fast_wave_bytes(D, SLOW);  // per-slot LDS scratch
+  const size_t slot = fast_wave_bytes(D, SLOW, LEAN);  // per-slot LDS scratch
   // waves per workgroup (<= 4): the most resident waves per CU under the
   // 160 KiB LDS of a gfx950 CU (the per-slot subset basis is D^2 doubles,
   // so at D = 50 only 2 waves fit; the smaller workgroup wins ties)
@@ -821,11 +857,11 @@ static int launch_pass_spw(sf_ctx* ctx, int it, const sf_fit_params* p,
   const size_t shm = shared + (size_t)nw * SPW * slot;
   if (shm > 64 * 1024)
     SF_HIP(hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&kl_fit_pass_kernel<SLOW, SPW>),
+        reinterpret_cast<const void*>(&kl_fit_pass_kernel<SLOW, SPW, LEAN>),
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
   int64_t blocks = (S + nw * SPW - 1) / (nw * SPW);
   if (blocks > 16384) blocks = 16384;
-  hipLaunchKernelGGL((kl_fit_pass_kernel<SLOW, SPW>), dim3((unsigned)blocks),
+  hipLaunchKernelGGL((kl_fit_pass_kernel<SLOW, SPW, LEAN>), dim3((unsigned)blocks),
                      dim3(64 * nw), shm, ctx->stream, it, p->niter, S, F, A, D,
                      phase, r.refph, r.sub, ctx->d_u, ctx->d_c, ctx->d_eig,
                      ctx->d_st_order, ctx->d_class, ctx->d_pos, ctx->d_ids,
@@ -843,12 +879,20 @@ template <bool SLOW>
 static int launch_pass(sf_ctx* ctx, int it, const sf_fit_params* p,
                        const RefSpec& r, int64_t S, int F, int A,
                        const double* phase, double* coef, double* resid,
-                       float* w_out, int32_t* order_out) {
-  if (!SLOW && ctx->D <= 32 && ctx->fit_pack)
-    return launch_pass_spw<SLOW, 2>(ctx, it, p, r, S, F, A, phase, coef, resid,
-                                    w_out, order_out);
-  return launch_pass_spw<SLOW, 1>(ctx, it, p, r, S, F, A, phase, coef, resid,
-                                  w_out, order_out);
+                       float* w_out, int32_t* order_out, bool lean) {
+  const bool pack = !SLOW && ctx->D <= 32 && ctx->fit_pack;
+  if (!SLOW && lean && ctx->fit_lean) {
+    if (pack)
+      return launch_pass_spw<false, 2, true>(ctx, it, p, r, S, F, A, phase, coef,
+                                             resid, w_out, order_out);
+    return launch_pass_spw<false, 1, true>(ctx, it, p, r, S, F, A, phase, coef,
+                                           resid, w_out, order_out);
+  }
+  if (pack)
+    return launch_pass_spw<SLOW, 2, false>(ctx, it, p, r, S, F, A, phase, coef,
+                                           resid, w_out, order_out);
+  return launch_pass_spw<SLOW, 1, false>(ctx, it, p, r, S, F, A, phase, coef, resid,
+                                         w_out, order_out);
 }
 
 int launch_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,
@@ -916,14 +960,14 @@ int launch_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,
   }
   if (!ctx->d_counters) {
     size_t c = 0;
-    SF_TRYF(grow(&ctx->d_counters, c, 4));
+    SF_TRYF(grow(&ctx->d_counters, c, 8));
   }
   SF_TRYF(ensure_pool(ctx, 1024));
   const int cap = (int)ctx->table_cap;
   SF_HIP(hipMemsetAsync(ctx->d_keys, 0, ctx->table_cap * sizeof(unsigned long long),
                         ctx->stream));
   SF_HIP(hipMemsetAsync(ctx->d_ids, 0xff, ctx->table_cap * sizeof(int), ctx->stream));
-  SF_HIP(hipMemsetAsync(ctx->d_counters, 0, 4 * sizeof(int), ctx->stream));
+  SF_HIP(hipMemsetAsync(ctx->d_counters, 0, 8 * sizeof(int), ctx->stream));
 
   {
     // lane groups of GW >= D lanes per slot, 4 waves per workgroup
@@ -947,13 +991,13 @@ int launch_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,
 
   const bool block_flags = p->screen_type != SF_SCREEN_PHASE;
   for (int it = 0; it < p->niter; ++it) {
-    int n_slow = 0;
-    SF_TRYF(number_and_decompose(ctx, &n_slow));
+    int n_slow = 0, n_nonuniform = 0;
+    SF_TRYF(number_and_decompose(ctx, &n_slow, &n_nonuniform));
     SF_TRYF(launch_pass<false>(ctx, it, p, r, S, F, A, phase, coef, resid,
-                               w_out, order_out));
+                               w_out, order_out, n_nonuniform == 0));
     if (n_slow > 0)
       SF_TRYF(launch_pass<true>(ctx, it, p, r, S, F, A, phase, coef, resid,
-                                w_out, order_out));
+                                w_out, order_out, false));
     if (block_flags && it + 1 < p->niter) {
       hipLaunchKernelGGL(kl_block_sigma_kernel, dim3(F * A), dim3(256), 0,
                          ctx->stream, T, F, A, D, phase, r.refph, r.sub,

@@ -74,7 +74,8 @@ struct sf_ctx {
   double* d_sigma = nullptr;             // [F][A] tec/amplitude block sigma
   size_t sigma_cap = 0;
   size_t slot_cap = 0;
-  int* d_counters = nullptr;  // [0] ids, [1] range start, [2] slow, [3] error
+  int* d_counters = nullptr;  // [0] ids, [1] range start, [2] slow, [3] error,
+                              // [4] non-uniform-weight slots
   double* d_scratch = nullptr;           // resid / state when caller passes NULL
   size_t scratch_cap = 0;
   float* d_wscratch = nullptr;
@@ -95,6 +96,7 @@ struct sf_ctx {
   int eval_groups = 0;          // SF_OPT_EVAL_GROUPS (0 = auto = 256)
   int eval_bands = 0;           // SF_OPT_EVAL_BANDS (0 = auto = 1)
   int fit_pack = 1;             // SF_OPT_FIT_PACK: 2 slots per wave for D <= 32
+  int fit_lean = 1;             // SF_OPT_FIT_LEAN: lean pass when weights are uniform
 };
 
 namespace sf {

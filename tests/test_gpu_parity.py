@@ -128,6 +128,24 @@ def test_fit_two_slots_per_wave_is_bit_identical(ctx, dev, name):
         assert np.array_equal(a.view(np.uint8), b.view(np.uint8))
 
 
+@pytest.mark.parametrize("name", ["synth20", "synth50", "synth12tiny", "fixture_kl"])
+def test_fit_lean_layout_is_bit_identical(ctx, dev, name):
+    """The lean pass layout (uniform weights: no per-slot G / subset-basis
+    copies in LDS, subset bases read from the pool) must not change a bit;
+    sets with unequal weights (synth12tiny) keep the general layout by the
+    classify count, so the two runs must agree there too."""
+    from ska_sdp_screen_fitting_amd._lib import SF_OPT_FIT_LEAN
+    g = load_golden(name)
+    lean = gpu_fit(ctx, dev, g)
+    ctx.set_option(SF_OPT_FIT_LEAN, 0)
+    try:
+        general = gpu_fit(ctx, dev, g)
+    finally:
+        ctx.set_option(SF_OPT_FIT_LEAN, 1)
+    for a, b in zip(lean, general):
+        assert np.array_equal(a.view(np.uint8), b.view(np.uint8))
+
+
 def test_fit_vs_oracle_config3_shape(ctx, dev):
     """A larger config-3-shaped synthetic (flags, outliers, adapted orders)."""
     from ska_sdp_screen_fitting_amd import geometry
