@@ -486,9 +486,25 @@ __global__ __launch_bounds__(256, SF_FIT_MINW) void kl_fit_pass_kernel(
 
   for (int64_t s = (int64_t)blockIdx.x * nslots + wv; s < S;
        s += (int64_t)gridDim.x * nslots) {
-    if (cls[s] != want) continue;
+    // the slot's independent loads go out together (class, mask position,
+    // phases, weights, state): checked one after another they were 4-5
+    // serial global round trips per slot, the pass's main cost.  The rare
+    // SLOW class tests its class first (it skips almost every slot).
+    if (SLOW && cls[s] != want) continue;
+    const uint8_t cl = SLOW ? want : cls[s];
     const int a = (int)(s % A);
     const int p0 = pos[s];
+    const int64_t base = s * D;
+    double phi_d = 0.0, w_d = 0.0, white_d = 0.0, resid_d = 0.0;
+    if (d < D) {
+      phi_d = phase_ref(phase, refph, ref_sub, s, a, A, D, d);
+      w_d = (double)w_out[base + d];
+      white_d = coef[base + d];
+      resid_d = resid[base + d];
+    }
+    double order = (double)order_out[s];
+    const double station_order = (double)st_order[a];
+    if (cl != want) continue;
     int id = -1;
     if (p0 >= 0) {
       id = ids[p0];
@@ -500,16 +516,6 @@ __global__ __launch_bounds__(256, SF_FIT_MINW) void kl_fit_pass_kernel(
       if (d == 0) atomicOr(counters + 3, 2);
       continue;
     }
-    const int64_t base = s * D;
-    double phi_d = 0.0, w_d = 0.0;
-    if (d < D) {
-      phi_d = phase_ref(phase, refph, ref_sub, s, a, A, D, d);
-      w_d = (double)w_out[base + d];
-    }
-    double white_d = (d < D) ? coef[base + d] : 0.0;
-    double resid_d = (d < D) ? resid[base + d] : 0.0;
-    double order = (double)order_out[s];
-    const double station_order = (double)st_order[a];
     const bool unfl = (d < D) && (w_d > 0.0);
     const unsigned long long um = G::ballot(unfl);
     const int n_unfl = __popcll(um);
