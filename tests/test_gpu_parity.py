@@ -165,6 +165,52 @@ def test_fit_vs_oracle_config3_shape(ctx, dev):
     np.testing.assert_allclose(resid, r["resid"], rtol=0, atol=1e-8)
 
 
+def test_fit_vs_oracle_max_directions(ctx, dev):
+    """D = SF_MAX_DIR (60, the ABI's limit): the largest k-step count, one
+    slot per wavefront, subset bases of up to 59 directions; orders and flags
+    identical to the oracle, coefficients within 1e-8."""
+    from ska_sdp_screen_fitting_amd import geometry
+    from ska_sdp_screen_fitting_amd._lib import SF_MAX_DIR
+    from ska_sdp_screen_fitting_amd.synthetic import make_solutions
+    s = make_solutions(n_ant=4, n_time=6, n_freq=2, n_dir=SF_MAX_DIR, seed=60,
+                       flag_frac=0.02, outlier_frac=0.01)
+    pp, _, _ = geometry.piercepoints(s.dir_radec)
+    ref = okl.reference_station(s.weight)
+    g = dict(val=s.val, weight=s.weight, ant_pos=s.ant_pos, piercepoints=pp,
+             ref_ant=ref, order=20)
+    coef, resid, w_out, orders = gpu_fit(ctx, dev, g)
+    r = okl.run_phase(s.val, s.weight, s.ant_pos, pp, ref, 20)
+    np.testing.assert_array_equal(orders, r["orders"])
+    np.testing.assert_array_equal(w_out, r["w_out"])
+    np.testing.assert_allclose(coef, r["coef"], rtol=0,
+                               atol=1e-8 * max(1.0, np.abs(r["coef"]).max()))
+    np.testing.assert_allclose(resid, r["resid"], rtol=0, atol=1e-8)
+
+
+def test_empty_and_out_of_range_inputs(ctx, dev):
+    """S = 0 writes nothing and succeeds (eval, eval_sums, tess_fill);
+    D > SF_MAX_DIR is refused with SF_EINVAL before any allocation."""
+    from ska_sdp_screen_fitting_amd._lib import SF_MAX_DIR, ScreenFitError
+    pp = np.stack([np.linspace(-900, 900, 6), np.linspace(300, -300, 6), np.zeros(6)], 1)
+    ctx.set_basis(pp)
+    x = np.linspace(-500, 500, 16)
+    ctx.set_grid(x, x)
+    coef = torch.zeros((1, 6), dtype=torch.float64, device=dev)
+    out = torch.full((1, 4, 16, 16), -7.0, dtype=torch.float32, device=dev)
+    sums = torch.zeros(1, dtype=torch.int32, device=dev)
+    ctx.eval(coef, 0, out, 1)
+    ctx.eval_sums(coef, 0, out, sums, 1)
+    labels = torch.ones((16, 16), dtype=torch.int32, device=dev)
+    ctx.tess_fill(labels, 16, 16, coef, 6, 0, out, 1)
+    torch.cuda.synchronize()
+    assert bool((out == -7.0).all()) and int(sums[0]) == 0
+    big = np.zeros((SF_MAX_DIR + 1, 3))
+    big[:, 0] = np.arange(SF_MAX_DIR + 1) * 10.0
+    with pytest.raises(ScreenFitError):
+        ctx.set_basis(big)
+    ctx.set_basis(pp)  # the context stays usable
+
+
 def test_fit_sharded_equals_unsharded(ctx, dev):
     """ant shards with the reference phases passed in (ref not local)."""
     g = load_golden("synth20")
@@ -221,7 +267,8 @@ def test_eval_128_vs_reference_golden(ctx, dev):
         np.testing.assert_allclose(out[:, 0:2], g["kl128"][k], rtol=0, atol=1e-6)
 
 
-@pytest.mark.parametrize("n_dir,grid", [(20, 256), (50, 64), (7, 17), (3, 40)])
+@pytest.mark.parametrize("n_dir,grid", [(20, 256), (50, 64), (7, 17), (3, 40),
+                                        (60, 48), (2, 16)])
 def test_eval_vs_oracle_sizes(ctx, dev, n_dir, grid):
     """Odd grids (scalar stores), every k-step count used by the configs."""
     from ska_sdp_screen_fitting_amd import geometry
