@@ -194,6 +194,31 @@ __device__ __forceinline__ unsigned row_sum16(unsigned v) {
   return v;
 }
 
+// Transposed sum of four per-lane partials p[r] (r = 0..3) over the 16 lanes
+// of each DPP row: lane i of the row returns the row total of p[i >> 2]
+// (every lane of quad i >> 2 gets it).  Halving the values at each of the
+// first two steps (exchange with lane i ^ 8, then with lane i ^ 7, keeping
+// the r the lane's bits 3, 2 name) costs 11 VALU ops instead of the 16 of
+// four row_sum16.
+__device__ __forceinline__ unsigned row_sum16_x4(const unsigned (&p)[4], int i) {
+  const bool b3 = i & 8, b2 = i & 4;
+  // step 1, partner i ^ 8 (row_ror:8): keep r in {2 b3, 2 b3 + 1}
+  const unsigned x0 = b3 ? p[0] : p[2], x1 = b3 ? p[1] : p[3];
+  const unsigned q0 = (b3 ? p[2] : p[0]) +
+                      (unsigned)__builtin_amdgcn_update_dpp(0, (int)x0, 0x128, 0xF, 0xF, false);
+  const unsigned q1 = (b3 ? p[3] : p[1]) +
+                      (unsigned)__builtin_amdgcn_update_dpp(0, (int)x1, 0x128, 0xF, 0xF, false);
+  // step 2, partner i ^ 7 (row_half_mirror: same bit 3, other bit 2): keep
+  // r = 2 b3 + b2; lane i now covers lanes {i, i^8, i^7, i^15}, and the four
+  // lanes of a quad cover the row
+  const unsigned w = b2 ? q0 : q1;
+  unsigned v = (b2 ? q1 : q0) +
+               (unsigned)__builtin_amdgcn_update_dpp(0, (int)w, 0x141, 0xF, 0xF, false);
+  v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // quad [1,0,3,2]
+  v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);  // quad [2,3,0,1]
+  return v;
+}
+
 template <bool NT>
 __device__ __forceinline__ void store4(float* p, v4f v) {
   if (NT) __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(p));
@@ -259,15 +284,18 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
     const bool scrub = flags & SF_EVAL_NAN_SCRUB;
     const bool be = flags & SF_EVAL_BIG_ENDIAN;
     const int64_t slot_base = sc * (int64_t)chunk_groups * 16;
-    // checksums: the slot sums of 4 consecutive groups of this wave are
-    // parked one per lane (lane 16 k + 4 gq + r <- slot row 4 r + k of the
-    // gq-th group) and leave as ONE 64-lane atomic instead of 16 (atomics run
-    // at the memory side, one wave-instruction per ~50 ns per CU)
+    // checksums: the slot sums of 4 groups of this wave are parked one per
+    // lane (lane 16 k + 4 r + gq <- slot row 4 r + k of the gq-th group, the
+    // layout row_sum16_x4 leaves) and leave as ONE 64-lane atomic instead of
+    // 16 (atomics run at the memory side, one wave-instruction per ~50 ns per
+    // CU); slots past S are never added
     unsigned pend = 0u;
     uint32_t pslot = ~0u;
     int gq = 0;
     auto flush_sums = [&]() {
-      if (pslot != ~0u) atomicAdd(sums + pslot, pend);
+      // phase screens on the float4 path sum planes 0 / 1 only (2 / 3 repeat
+      // them): doubled here, once per flush instead of once per row
+      if (pslot < (uint32_t)S) atomicAdd(sums + pslot, (VEC4 && !GAIN) ? 2u * pend : pend);
       pend = 0u;
       pslot = ~0u;
       gq = 0;
@@ -315,6 +343,8 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
             accy[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ay[kk], bval(kk, t), accy[t], 0, 0, 0);
           }
       }
+      // this lane's checksum partial of each of its 4 slot rows
+      unsigned part[4] = {0u, 0u, 0u, 0u};
       // one MFMA accumulator row: 4 slot rows x this lane's 4 pixels; BE
       // (FITS byte order) as a compile-time branch of the whole row
       auto row_out = [&](int r, auto be_tag) {
@@ -380,11 +410,11 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
             }
             if (sums) {
               // phase screens store (cos, sin) twice: sum the planes once
+              // (the flush doubles the total)
 #pragma unroll
               for (int q = 0; q < (GAIN ? 4 : 2); ++q)
 #pragma unroll
                 for (int t = 0; t < kTiles; ++t) cs += fbits(pv[q][t]);
-              if (!GAIN) cs *= 2u;
             }
           }
         } else {
@@ -399,14 +429,7 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
             }
           }
         }
-        if (sums) {
-          // the 16 lanes of this slot row (one DPP row) hold its 64 pixels
-          cs = row_sum16(cs);
-          if ((l & 15) == 4 * gq + r) {
-            pend = cs;
-            pslot = (uint32_t)s;
-          }
-        }
+        if (sums) part[r] = cs;  // the 16 lanes of the row sum it below
       };
       if (be) {
 #pragma unroll
@@ -415,7 +438,14 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
 #pragma unroll
         for (int r = 0; r < 4; ++r) row_out(r, std::false_type{});
       }
-      if (sums && ++gq == 4) flush_sums();
+      if (sums) {
+        const unsigned tot = row_sum16_x4(part, l & 15);
+        if ((l & 3) == gq) {
+          pend = tot;
+          pslot = (uint32_t)(s0 + 4 * ((l >> 2) & 3) + (l >> 4));
+        }
+        if (++gq == 4) flush_sums();
+      }
     }
     if (sums) flush_sums();
   }  // workgroup walk
