@@ -99,14 +99,25 @@ def parse():
     ap.add_argument("--checksum", default="auto", choices=("auto", "on", "off"),
                     help="per-slot output checksums (sf_kl_eval_sums); auto: on "
                          "for config4 / config5, whose cubes are discarded")
-    ap.add_argument("--screen", default="phase", choices=("phase", "gain"),
+    ap.add_argument("--smooth-pix", type=float, default=0.0,
+                    help="--screen tess: Gaussian sigma in pixels (<= 6: "
+                         "fused in the fill kernel); 0 = make_aterm_image's "
+                         "default smooth_deg = 0")
+    ap.add_argument("--screen", default="phase", choices=("phase", "gain", "tess"),
                     help="gain: phase + slow XX / YY amplitude screens "
                          "(kl_screen.py:96-125, 319-378): per step the phase "
                          "fit and the two log10-amplitude fits (niter 3, "
                          "block sigma over all times, so one time chunk), "
-                         "then the three-contraction gain evaluation")
+                         "then the three-contraction gain evaluation; "
+                         "tess: the tessellated (Voronoi) fill of every slot "
+                         "(voronoi_screen.py:132-216, sf_tess_fill), no fit")
     ap.add_argument("--eval-only", action="store_true",
                     help="time only sf_kl_eval (profiling)")
+    ap.add_argument("--as-shard-of", type=int, default=0,
+                    help="strong workloads, one process: run the shard rank 0 "
+                         "of an N-way split would run (per-GPU throughput of "
+                         "an N-GPU job measured on one GPU; the line's value is "
+                         "then the shard's own slots/s, see 'projection')")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="gloo: rehearse N ranks on a 1-GPU box (setup "
                          "collectives on the CPU, ranks share the device)")
@@ -372,6 +383,105 @@ def side_legs(ctx, torch, dev, stream, fit_stream, fit, evaluate, coef, bounds,
     return res
 
 
+def tess_steps(args, ctx, torch, dev, dist, world, rank, coll_dev, sol, setup,
+               A_total, strong):
+    """--screen tess: one step = the tessellated fill (gather of the
+    referenced per-direction cos / sin by the Voronoi label raster, optional
+    fused Gaussian) of every slot of the rank into the HBM ring; the label
+    template is built once on the host (voronoi_screen.py:218-351)."""
+    from ska_sdp_screen_fitting_amd._lib import SF_EVAL_NAN_SCRUB
+    from ska_sdp_screen_fitting_amd.synthetic import (FIELD_DEC_DEG,
+                                                      FIELD_RA_DEG,
+                                                      FIELD_WIDTH_DEG)
+    from ska_sdp_screen_fitting_amd.voronoi_screen import tessellation_template
+    A, T, F, D, N, cell = WORKLOADS[args.workload]
+    T, F, A, D = sol.val.shape
+    lab, _ = tessellation_template(np.rad2deg(sol.dir_radec.astype(np.float64)),
+                                   FIELD_RA_DEG, FIELD_DEC_DEG, FIELD_WIDTH_DEG, cell)
+    assert lab.shape == (N, N)
+    S, P = T * F * A, N * N
+    lab_d = torch.from_numpy(np.ascontiguousarray(lab, np.int32)).to(dev)
+    # referenced phases (stationscreen.py:994-997), the fill's input
+    ph = (torch.from_numpy(sol.val).to(dev)
+          - setup["ref_phase"].to(dev)[:, :, None, :]).reshape(S, D).contiguous()
+    ring = int(min(S, max(1, args.ring_gb * 2 ** 30 // (16 * P))))
+    out = torch.empty((ring, 4, N, N), dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    ctx.set_stream(stream.cuda_stream)
+    flags = SF_EVAL_NAN_SCRUB
+
+    def step():
+        ctx.tess_fill(lab_d, N, N, ph, D, S, out, ring_slots=ring,
+                      smooth_pix=args.smooth_pix, flags=flags)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    evs = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        step()
+        e1.record(stream)
+        evs.append((e0, e1))
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
+    if world > 1:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    elapsed = tmax.item()
+    launch_s = float(np.mean([a.elapsed_time(b) for a, b in evs])) * 1e-3
+    # parity spot check of the last ring slots (not timed): cos^2 + sin^2 = 1
+    # without smoothing (unit amplitudes), and the first slot vs a gather
+    chk = out[: min(ring, 16)].double()
+    unit_err = (float((chk[:, 0] ** 2 + chk[:, 1] ** 2 - 1).abs().max())
+                if args.smooth_pix == 0 else None)
+    one = torch.empty((1, 4, N, N), dtype=torch.float32, device=dev)
+    ctx.tess_fill(lab_d, N, N, ph[:1], D, 1, one, smooth_pix=0.0, flags=flags)
+    p0 = ph[0].cpu().numpy()
+    want = np.stack([np.cos(p0), np.sin(p0), np.cos(p0), np.sin(p0)]).astype(np.float32)
+    want = want[:, lab - 1]
+    got = one[0].cpu().numpy()
+    ulp = int(np.abs(got.view(np.int32).astype(np.int64) - want.view(np.int32)).max())
+    if rank == 0:
+        bytes_launch = S * (16 * P + 8 * D)
+        achieved = bytes_launch / launch_s / 1e9
+        kernel = "kl_tess_gather_kernel" if args.smooth_pix == 0 else "kl_tess_kernel"
+        line = {
+            "metric": METRIC,
+            "value": T * F * (A if args.as_shard_of else A_total) * args.steps / elapsed,
+            "unit": "screen-slots/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong" if strong else "weak",
+            "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {
+                "workload": (f"{args.workload}-tess: {A_total} ant x {T} time x {F} "
+                             f"freq x {D} dir, {A} ant per GPU, tessellated "
+                             f"(Voronoi) {N}^2 screen, smooth {args.smooth_pix} px"),
+                "screen": "tess", "slots_per_gpu": S, "grid": N, "n_dir": D,
+                "parallelism": f"ant-shard x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": None, "kernel": kernel,
+                         "bytes_per_launch": bytes_launch,
+                         "launch_ms": launch_s * 1e3},
+            "check": {"max_abs_cos2_plus_sin2_minus_1": unit_err,
+                      "slot0_max_ulp_vs_numpy_gather": ulp},
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     import torch
@@ -412,7 +522,9 @@ def main():
     if strong:
         from ska_sdp_screen_fitting_amd.distributed import shard_range
         A_total = A
-        a0, a1 = shard_range(A_total, world, rank)
+        if args.as_shard_of and world != 1:
+            raise SystemExit("--as-shard-of is a one-process projection")
+        a0, a1 = shard_range(A_total, args.as_shard_of or world, rank)
         A = a1 - a0
     else:
         A_total, a0 = A * world, A * rank
@@ -424,6 +536,9 @@ def main():
     assert len(setup["x"]) == N
 
     ctx = get_context(gpu)
+    if args.screen == "tess":
+        return tess_steps(args, ctx, torch, dev, dist, world, rank, coll_dev,
+                          sol, setup, A_total, strong)
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)
     ctx.set_basis(setup["piercepoints"], 100, 5.0 / 3.0)
@@ -646,7 +761,7 @@ def main():
         ceil = side.get("store_ceiling") if side else None
         line = {
             "metric": METRIC,
-            "value": T * F * A_total * args.steps / elapsed,
+            "value": T * F * (A if args.as_shard_of else A_total) * args.steps / elapsed,
             "unit": "screen-slots/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -696,6 +811,15 @@ def main():
         }
         if side:
             line["side_legs"] = side
+        if args.as_shard_of:
+            # one GPU running the shard of rank 0 of an N-way strong split:
+            # nothing in the timed step is shared between ranks, so N such
+            # GPUs would process N x this (the driver measures the real curve)
+            line["projection"] = {
+                "as_shard_of": args.as_shard_of,
+                "shard_slots_per_s": line["value"],
+                "aggregate_if_n_gpus": line["value"] * args.as_shard_of,
+                "note": "one process, rank 0's shard; not an N-GPU measurement"}
         # the fit (slots/s and achieved fp64 FLOP/s): alone
         # on the whole chip (side leg) and per kernel from PMC passes
         fe = _profile_entry("fit_flops.json", wkey, "fit")

@@ -40,6 +40,25 @@ __device__ __forceinline__ float rev_reduce(double rev, bool scrub) {
   return (scrub && __builtin_isnan(f)) ? 0.0f : f;
 }
 
+// rev_reduce of N (2 or 4) phases at once: v_cmp_u of a PAIR flags either
+// being NaN, so N / 2 compares collect a lane flag and the N selects run only
+// when some lane of the wave has a NaN (a wave-uniform branch; same bits as N
+// rev_reduce calls)
+template <int N>
+__device__ __forceinline__ void rev_reduce_n(float (&f)[N], const double (&rev)[N],
+                                             bool scrub) {
+  static_assert(N % 2 == 0, "pairs");
+  bool bad = false;
+#pragma unroll
+  for (int t = 0; t < N; ++t) f[t] = (float)(rev[t] - rint(rev[t]));
+#pragma unroll
+  for (int t = 0; t < N; t += 2) bad |= __builtin_isunordered(f[t], f[t + 1]);
+  if (scrub && __builtin_amdgcn_ballot_w64(bad) != 0) {
+#pragma unroll
+    for (int t = 0; t < N; ++t) f[t] = __builtin_isnan(f[t]) ? 0.0f : f[t];
+  }
+}
+
 // v_sin_f32 / v_cos_f32 return NaN for a NaN argument (checked by the
 // unscrubbed cases of tests/test_gpu_parity.py::test_eval_kernels_agree)
 __device__ __forceinline__ void sincos_rev(float f, float& s, float& c) {
@@ -360,6 +379,21 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
         }
         // planes 0..3 = Re XX, Im XX, Re YY, Im YY
         float pv[4][kTiles];
+        // per-value NaN scrub (gain, fp64 sincos): v_cmp_u of a PAIR of
+        // values flags either being NaN, so 2 compares per pixel collect a
+        // lane flag, and the 8 selects per pixel run only when some lane of
+        // the wave has a NaN (a wave-uniform branch; same bits either way)
+        constexpr bool kScrubValues = GAIN || !FAST;
+        bool bad = false;
+        // phase screens, fast epilogue: the reduced arguments of the 4 tiles
+        // first, NaN scrubbed together (cos 1, sin 0)
+        float fr[kTiles];
+        if constexpr (FAST && !GAIN) {
+          double rv[kTiles];
+#pragma unroll
+          for (int t = 0; t < kTiles; ++t) rv[t] = acc[t][r];
+          rev_reduce_n<kTiles>(fr, rv, scrub);
+        }
 #pragma unroll
         for (int t = 0; t < kTiles; ++t) {
           float sf, cf;
@@ -386,16 +420,27 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
             }
           } else {
             // FAST: NaN scrubbed on the reduced argument (cos 1, sin 0)
-            jones_sincos<FAST>(acc[t][r], sf, cf, scrub);
+            if constexpr (FAST && !GAIN) sincos_rev(fr[t], sf, cf);
+            else jones_sincos<FAST>(acc[t][r], sf, cf, scrub);
             pv[0][t] = pv[2][t] = cf;
             pv[1][t] = pv[3][t] = sf;
           }
+          if (kScrubValues)
+            bad |= __builtin_isunordered(pv[0][t], pv[1][t]) |
+                   __builtin_isunordered(pv[2][t], pv[3][t]);
+        }
+        if (kScrubValues && scrub && __builtin_amdgcn_ballot_w64(bad) != 0) {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            if (scrub && (GAIN || !FAST) && isnan(pv[q][t]))
-              pv[q][t] = (q & 1) ? 0.0f : 1.0f;
-            if (kBE) pv[q][t] = bswapf(pv[q][t]);
-          }
+          for (int t = 0; t < kTiles; ++t)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              if (isnan(pv[q][t])) pv[q][t] = (q & 1) ? 0.0f : 1.0f;
+        }
+        if (kBE) {
+#pragma unroll
+          for (int t = 0; t < kTiles; ++t)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) pv[q][t] = bswapf(pv[q][t]);
         }
         float* o = out + ((int64_t)so * 4) * P + p0;
         unsigned cs = 0u;
@@ -544,8 +589,10 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float red[TPW];
+        double rv[TPW];
 #pragma unroll
-        for (int t = 0; t < TPW; ++t) red[t] = rev_reduce(acc[t][r], scrub);
+        for (int t = 0; t < TPW; ++t) rv[t] = acc[t][r];
+        rev_reduce_n<TPW>(red, rv, scrub);
         float* dst = &buf[acc_row(l, r)][wblk * kWavePix + (l & 15) * kTiles + t0];
         if (TPW == 4)
           *reinterpret_cast<v4f*>(dst) = v4f{red[0], red[1], red[2 % TPW], red[3 % TPW]};

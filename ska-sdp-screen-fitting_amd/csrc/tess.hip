@@ -124,6 +124,88 @@ __global__ __launch_bounds__(256) void kl_tess_kernel(
   }
 }
 
+// Unsmoothed fill (R = 0, the make_aterm_image default smooth_deg = 0): a
+// pure gather-store, laid out for HBM writes.  A workgroup owns a run of
+// kGatherRun consecutive pixels (4 per lane, 1 KiB per wave and plane) and a
+// chunk of kGatherSlots slots: it first builds the chunk's value table in LDS
+// -- per (slot, direction) the float4 {A_xx cos, A_xx sin, A_yy cos, A_yy
+// sin} with the NaN scrub and the byte swap already applied (the output IS
+// the table entry when nothing is smoothed, so scrubbing the entry equals
+// scrubbing the pixel) -- keeps its 4 labels in registers, and then per slot
+// reads 4 table entries (ds_read_b128) and writes 4 float4 stores, one per
+// plane: 4 KiB contiguous runs per (slot, plane) per workgroup.  Same fp64
+// sincos and casts as kl_tess_kernel, so the same bits.
+constexpr int kGatherWaves = 4;
+constexpr int kGatherRun = 64 * 4 * kGatherWaves;  // pixels per workgroup
+constexpr int kGatherSlots = 32;                   // slots per work item
+
+template <bool VEC4>
+__global__ __launch_bounds__(64 * kGatherWaves) void kl_tess_gather_kernel(
+    const int32_t* __restrict__ labels, int64_t P,
+    const double* __restrict__ phase, const double* __restrict__ amp_xx,
+    const double* __restrict__ amp_yy, int D, int64_t S,
+    float* __restrict__ out, int64_t ring, int64_t n_pb, int64_t n_sc,
+    unsigned flags) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  extern __shared__ v4f gtab[];  // [kGatherSlots][D + 1]
+  const int DT = D + 1;          // entry D: invalid labels (NaN / scrubbed)
+  const bool scrub = flags & SF_EVAL_NAN_SCRUB;
+  const bool be = flags & SF_EVAL_BIG_ENDIAN;
+  auto fin = [&](float x, int p) {
+    if (scrub && isnan(x)) x = (p & 1) ? 0.0f : 1.0f;
+    if (be) x = __uint_as_float(__builtin_bswap32(__float_as_uint(x)));
+    return x;
+  };
+  for (int64_t bb = blockIdx.x; bb < n_pb * n_sc; bb += gridDim.x) {
+    const int64_t pb = bb % n_pb, sc = bb / n_pb;
+    const int64_t s0 = sc * kGatherSlots;
+    const int ns = (int)((S - s0) < kGatherSlots ? (S - s0) : kGatherSlots);
+    __syncthreads();  // the previous item's table reads are done
+    for (int e = threadIdx.x; e < ns * DT; e += blockDim.x) {
+      const int k = e / DT, d = e - k * DT;
+      v4f v;
+      if (d < D) {
+        const int64_t i = (s0 + k) * D + d;
+        double sn, cn;
+        sincos(phase[i], &sn, &cn);
+        const double ax = amp_xx ? amp_xx[i] : 1.0;
+        const double ay = amp_yy ? amp_yy[i] : ax;
+        v = v4f{(float)(ax * cn), (float)(ax * sn), (float)(ay * cn), (float)(ay * sn)};
+      } else {
+        const float q = __builtin_nanf("");
+        v = v4f{q, q, q, q};
+      }
+      gtab[e] = v4f{fin(v[0], 0), fin(v[1], 1), fin(v[2], 2), fin(v[3], 3)};
+    }
+    __syncthreads();
+    const int64_t p0 = pb * kGatherRun + 4 * (int64_t)threadIdx.x;
+    if (p0 >= P) continue;  // after the barrier: nothing below syncs
+    int lab[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int lb = (p0 + j < P) ? labels[p0 + j] - 1 : 0;
+      lab[j] = (lb >= 0 && lb < D) ? lb : D;
+    }
+    for (int k = 0; k < ns; ++k) {
+      const v4f* t = gtab + k * DT;
+      const v4f a = t[lab[0]], b = t[lab[1]], c = t[lab[2]], d = t[lab[3]];
+      float* o = out + ((s0 + k) % ring) * 4 * P + p0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (VEC4) {
+          __builtin_nontemporal_store(v4f{a[q], b[q], c[q], d[q]},
+                                      reinterpret_cast<v4f*>(o + q * P));
+        } else {
+          const float v[4] = {a[q], b[q], c[q], d[q]};
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (p0 + j < P) o[q * P + j] = v[j];
+        }
+      }
+    }
+  }
+}
+
 // Separable Gaussian of Screen.write for any radius (screen.py:353-362:
 // scipy.ndimage.gaussian_filter(img, sigma=(0, s, s)) per (time, freq,
 // station), i.e. per image of the [.][4][ny][nx] cube): one 1-D pass per
@@ -201,6 +283,26 @@ int launch_tess(sf_ctx* ctx, const int32_t* labels, int nx, int ny,
                 const double* phase, const double* amp_xx,
                 const double* amp_yy, int D, int64_t S, float* out,
                 int64_t ring, const double* d_w, int R, unsigned flags) {
+  if (R == 0) {
+    const int64_t P = (int64_t)nx * ny;
+    const int64_t n_pb = (P + kGatherRun - 1) / kGatherRun;
+    const int64_t n_sc = (S + kGatherSlots - 1) / kGatherSlots;
+    int64_t grid = n_pb * n_sc;
+    const int64_t cap = ((int64_t)1 << 31) / (64 * kGatherWaves);
+    if (grid > cap) grid = cap;  // workgroups walk the remaining items
+    const size_t lds = (size_t)kGatherSlots * (D + 1) * 4 * sizeof(float);
+    const bool vec4 = (P % 4 == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
+    if (vec4)
+      hipLaunchKernelGGL(kl_tess_gather_kernel<true>, dim3((unsigned)grid),
+                         dim3(64 * kGatherWaves), lds, ctx->stream, labels, P,
+                         phase, amp_xx, amp_yy, D, S, out, ring, n_pb, n_sc, flags);
+    else
+      hipLaunchKernelGGL(kl_tess_gather_kernel<false>, dim3((unsigned)grid),
+                         dim3(64 * kGatherWaves), lds, ctx->stream, labels, P,
+                         phase, amp_xx, amp_yy, D, S, out, ring, n_pb, n_sc, flags);
+    SF_HIP(hipGetLastError());
+    return SF_OK;
+  }
   const int tiles = ((nx + kTT - 1) / kTT) * ((ny + kTT - 1) / kTT);
   const int64_t chunks = (S + kTessSlots - 1) / kTessSlots;
   hipLaunchKernelGGL(kl_tess_kernel, dim3(tiles, (unsigned)chunks), dim3(256),

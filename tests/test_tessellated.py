@@ -160,7 +160,8 @@ def _tess_gpu(lab, phase, smooth):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cell,smooth", [(0.2, 0.0), (0.2, 0.5), (0.05, 1.3),
-                                         (0.02602, 4.0), (0.02602, 10.0)])
+                                         (0.02602, 4.0), (0.02602, 10.0),
+                                         (0.05, 0.0), (0.02602, 0.0)])
 def test_tess_kernel_vs_oracle(cell, smooth):
     """Fused gather + Gaussian (smooth <= 6 px) and, at 10 px (radius 40),
     gather then the separable passes of sf_smooth -- both vs scipy."""
@@ -270,3 +271,48 @@ def test_tess_rejects_bad_labels():
     lab[3, 3] = 4
     with pytest.raises(ValueError):
         _tess_gpu(lab, np.zeros((2, 3)), 0.0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,S", [(17, 70), (128, 45), (64, 33), (33, 1)])
+def test_tess_gather_amplitudes_nan_byteswap(n, S):
+    """The unsmoothed gather-store kernel (float4 runs when n^2 % 4 == 0,
+    scalar tail otherwise; slot chunks of 32): gain tables A cos / A sin,
+    NaN phases and amplitudes (scrubbed to 1 / 0, or left NaN), FITS byte
+    order -- vs fp64 numpy cast once to fp32 (<= 1 ulp)."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from ska_sdp_screen_fitting_amd import get_context
+    from ska_sdp_screen_fitting_amd._lib import SF_EVAL_BIG_ENDIAN, SF_EVAL_NAN_SCRUB
+    dev = torch.device("cuda", 0)
+    ctx = get_context(0)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    rng = np.random.default_rng(n * 1000 + S)
+    D = 9
+    lab = rng.integers(1, D + 1, size=(n, n)).astype(np.int32)
+    ph = rng.uniform(-20.0, 20.0, size=(S, D))
+    ax = 10.0 ** rng.normal(0.0, 0.3, size=(S, D))
+    ay = 10.0 ** rng.normal(0.0, 0.3, size=(S, D))
+    ph[S // 2, 3] = np.nan
+    ax[S - 1, 5] = np.nan
+    tab = np.stack([ax * np.cos(ph), ax * np.sin(ph), ay * np.cos(ph),
+                    ay * np.sin(ph)], axis=-1).astype(np.float32)  # [S][D][4]
+    want = np.moveaxis(tab[:, lab - 1, :], -1, 1)  # [S][4][n][n]
+    d = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev)
+         for k, v in (("lab", lab), ("ph", ph), ("ax", ax), ("ay", ay))}
+    for flags in (SF_EVAL_NAN_SCRUB, SF_EVAL_NAN_SCRUB | SF_EVAL_BIG_ENDIAN, 0):
+        out = torch.full((S, 4, n, n), -5.0, dtype=torch.float32, device=dev)
+        ctx.tess_fill(d["lab"], n, n, d["ph"], D, S, out, amp_xx=d["ax"],
+                      amp_yy=d["ay"], smooth_pix=0.0, flags=flags)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        if flags & SF_EVAL_BIG_ENDIAN:
+            got = got.byteswap()
+        exp = _scrub(want) if flags & SF_EVAL_NAN_SCRUB else want
+        nan = np.isnan(exp)
+        assert np.array_equal(np.isnan(got), nan)
+        if flags & SF_EVAL_NAN_SCRUB:
+            assert not nan.any()
+        diff = np.abs(got.view(np.int32).astype(np.int64) - exp.view(np.int32))
+        assert diff[~nan].max() <= 1
