@@ -99,6 +99,12 @@ def parse():
     ap.add_argument("--checksum", default="auto", choices=("auto", "on", "off"),
                     help="per-slot output checksums (sf_kl_eval_sums); auto: on "
                          "for config4 / config5, whose cubes are discarded")
+    ap.add_argument("--tess-slots", type=int, default=0,
+                    help="SF_OPT_TESS_SLOTS: slots per work item of the "
+                         "unsmoothed tessellated fill (0 = library default)")
+    ap.add_argument("--tess-waves", type=int, default=0,
+                    help="SF_OPT_TESS_WAVES: waves per workgroup of the "
+                         "unsmoothed tessellated fill (0 = library default)")
     ap.add_argument("--smooth-pix", type=float, default=0.0,
                     help="--screen tess: Gaussian sigma in pixels (<= 6: "
                          "fused in the fill kernel); 0 = make_aterm_image's "
@@ -389,7 +395,8 @@ def tess_steps(args, ctx, torch, dev, dist, world, rank, coll_dev, sol, setup,
     referenced per-direction cos / sin by the Voronoi label raster, optional
     fused Gaussian) of every slot of the rank into the HBM ring; the label
     template is built once on the host (voronoi_screen.py:218-351)."""
-    from ska_sdp_screen_fitting_amd._lib import SF_EVAL_NAN_SCRUB
+    from ska_sdp_screen_fitting_amd._lib import (SF_EVAL_NAN_SCRUB, SF_OPT_TESS_SLOTS,
+                                                 SF_OPT_TESS_WAVES)
     from ska_sdp_screen_fitting_amd.synthetic import (FIELD_DEC_DEG,
                                                       FIELD_RA_DEG,
                                                       FIELD_WIDTH_DEG)
@@ -408,6 +415,10 @@ def tess_steps(args, ctx, torch, dev, dist, world, rank, coll_dev, sol, setup,
     out = torch.empty((ring, 4, N, N), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)
+    if args.tess_slots:
+        ctx.set_option(SF_OPT_TESS_SLOTS, args.tess_slots)
+    if args.tess_waves:
+        ctx.set_option(SF_OPT_TESS_WAVES, args.tess_waves)
     flags = SF_EVAL_NAN_SCRUB
 
     def step():

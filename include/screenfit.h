@@ -149,6 +149,13 @@ int sf_device_cus(sf_ctx* ctx, int* n_cu);
  * read their subset basis from the pool), for 2.7-4x the resident waves.
  * Same results bit for bit; 0 forces the general layout. */
 #define SF_OPT_FIT_LEAN 10
+/* SF_OPT_TESS_SLOTS = n (0 = auto 16, else 1..256): slots per work item of
+ * the unsmoothed tessellated fill (the item's value-table slice sits in
+ * LDS); SF_OPT_TESS_WAVES = 4, 8 or 16 (0 = auto 16): its waves per
+ * workgroup, each writing whole 4 KiB runs of its own slots.  Outputs are
+ * identical for every setting. */
+#define SF_OPT_TESS_SLOTS 11
+#define SF_OPT_TESS_WAVES 12
 #define SF_EVAL_KERNEL_AUTO 0
 #define SF_EVAL_KERNEL_TILE 1
 #define SF_EVAL_KERNEL_LDS4 2

@@ -101,6 +101,7 @@ int sf_destroy(sf_ctx* ctx) {
   hipFree(ctx->d_oscratch);
   hipFree(ctx->d_gw);
   hipFree(ctx->d_smooth);
+  hipFree(ctx->d_tess_tab);
   delete ctx;
   return SF_OK;
 }
@@ -191,6 +192,16 @@ int sf_set_option(sf_ctx* ctx, int option, int value) {
       SF_REQUIRE(value >= 0 && value <= 128 && (value & (value - 1)) == 0,
                  SF_EINVAL, "sf_set_option: bands must be 0 or a power of two <= 128");
       ctx->eval_bands = value;
+      return SF_OK;
+    case SF_OPT_TESS_SLOTS:
+      SF_REQUIRE(value >= 0 && value <= 256, SF_EINVAL,
+                 "sf_set_option: tess slots must be 0..256");
+      ctx->tess_slots = value;
+      return SF_OK;
+    case SF_OPT_TESS_WAVES:
+      SF_REQUIRE(value == 0 || value == 4 || value == 8 || value == 16, SF_EINVAL,
+                 "sf_set_option: tess waves must be 0, 4, 8 or 16");
+      ctx->tess_waves = value;
       return SF_OK;
     case SF_OPT_EVAL_MAX_BLOCKS:
       SF_REQUIRE(value >= 0, SF_EINVAL, "sf_set_option: negative block cap");
@@ -481,7 +492,8 @@ int sf_tess_fill(sf_ctx* ctx, const int32_t* labels, int nx, int ny,
                  const double* amp_yy, int D, int64_t S, float* out,
                  int64_t ring, double smooth_pix, unsigned flags) {
   SF_REQUIRE(ctx && labels && phase && out, SF_EINVAL, "sf_tess_fill: NULL argument");
-  SF_REQUIRE(nx >= 1 && ny >= 1 && D >= 1 && D <= 64 && S >= 0 && ring >= 1,
+  SF_REQUIRE(nx >= 1 && ny >= 1 && D >= 1 && D <= 64 && S >= 0 && ring >= 1 &&
+                 ring <= INT32_MAX,
              SF_EINVAL, "sf_tess_fill: bad shape");
   SF_REQUIRE(smooth_pix >= 0.0 && smooth_pix <= 1e4, SF_EINVAL,
              "sf_tess_fill: smooth_pix must be in [0, 1e4]");

@@ -85,6 +85,8 @@ struct sf_ctx {
   size_t gw_cap = 0;                     // doubles
   float* d_smooth = nullptr;
   size_t smooth_cap = 0;                 // bytes
+  float* d_tess_tab = nullptr;           // tessellated value table [S][D+1][4]
+  size_t tess_tab_cap = 0;               // bytes
   // fast-path switch (SCREENFIT_FIT=general forces the general kernel)
   int force_general = 0;
   // evaluation kernel (SF_OPT_EVAL_KERNEL)
@@ -95,6 +97,8 @@ struct sf_ctx {
   int eval_xcd_map = -1;        // SF_OPT_EVAL_XCD_MAP (-1 = auto)
   int eval_groups = 0;          // SF_OPT_EVAL_GROUPS (0 = auto = 256)
   int eval_bands = 0;           // SF_OPT_EVAL_BANDS (0 = auto = 1)
+  int tess_slots = 0;           // SF_OPT_TESS_SLOTS (0 = auto = 16)
+  int tess_waves = 0;           // SF_OPT_TESS_WAVES (0 = auto = 16)
   int fit_pack = 1;             // SF_OPT_FIT_PACK: 2 slots per wave for D <= 32
   int fit_lean = 1;             // SF_OPT_FIT_LEAN: lean pass when weights are uniform
 };

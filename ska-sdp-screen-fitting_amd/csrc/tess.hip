@@ -125,83 +125,118 @@ __global__ __launch_bounds__(256) void kl_tess_kernel(
 }
 
 // Unsmoothed fill (R = 0, the make_aterm_image default smooth_deg = 0): a
-// pure gather-store, laid out for HBM writes.  A workgroup owns a run of
-// kGatherRun consecutive pixels (4 per lane, 1 KiB per wave and plane) and a
-// chunk of kGatherSlots slots: it first builds the chunk's value table in LDS
-// -- per (slot, direction) the float4 {A_xx cos, A_xx sin, A_yy cos, A_yy
-// sin} with the NaN scrub and the byte swap already applied (the output IS
-// the table entry when nothing is smoothed, so scrubbing the entry equals
-// scrubbing the pixel) -- keeps its 4 labels in registers, and then per slot
-// reads 4 table entries (ds_read_b128) and writes 4 float4 stores, one per
-// plane: 4 KiB contiguous runs per (slot, plane) per workgroup.  Same fp64
-// sincos and casts as kl_tess_kernel, so the same bits.
-constexpr int kGatherWaves = 4;
-constexpr int kGatherRun = 64 * 4 * kGatherWaves;  // pixels per workgroup
-constexpr int kGatherSlots = 32;                   // slots per work item
+// pure gather-store, laid out for HBM writes, in two kernels.
+//  * kl_tess_table_kernel: per (slot, direction) the float4 {A_xx cos, A_xx
+//    sin, A_yy cos, A_yy sin} (fp64 sincos and products, one cast -- the
+//    bits of kl_tess_kernel) with the NaN scrub and the byte swap already
+//    applied (the output IS the table entry when nothing is smoothed, so
+//    scrubbing the entry equals scrubbing the pixel), plus entry D for
+//    labels outside 1..D: once per slot instead of once per (slot, pixel
+//    block).  [S][D + 1] float4 in a context scratch buffer.
+//  * kl_tess_gather_kernel: a workgroup owns a run of kGatherRun consecutive
+//    pixels and a chunk of slots; it copies the chunk's table slice to LDS,
+//    and each wave takes every NW-th slot of the chunk over the
+//    whole run (16 labels per lane in registers): per slot 16 entry reads
+//    (ds_read_b128) and 16 float4 stores, i.e. one wave writes a 4 KiB
+//    contiguous run per (slot, plane) -- the LDS-staged eval's store shape.
+constexpr int kGatherRun = 1024;       // pixels per workgroup (4 KiB per plane)
+// one slot per wave per work item, 16 waves: 0.816 of 8 TB/s at 256^2 x
+// 102,400 slots vs 0.73-0.77 for 4 / 8 waves or 2+ slots per wave
+// (profiles/round2zd_tess_gather_sweep.txt)
+constexpr int kGatherWavesAuto = 16;   // waves per workgroup (SF_OPT_TESS_WAVES)
+constexpr int kGatherSlotsAuto = 16;   // slots per work item (SF_OPT_TESS_SLOTS)
 
-template <bool VEC4>
-__global__ __launch_bounds__(64 * kGatherWaves) void kl_tess_gather_kernel(
-    const int32_t* __restrict__ labels, int64_t P,
+typedef float tess_v4f __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void kl_tess_table_kernel(
     const double* __restrict__ phase, const double* __restrict__ amp_xx,
     const double* __restrict__ amp_yy, int D, int64_t S,
-    float* __restrict__ out, int64_t ring, int64_t n_pb, int64_t n_sc,
-    unsigned flags) {
-  typedef float v4f __attribute__((ext_vector_type(4)));
-  extern __shared__ v4f gtab[];  // [kGatherSlots][D + 1]
-  const int DT = D + 1;          // entry D: invalid labels (NaN / scrubbed)
-  const bool scrub = flags & SF_EVAL_NAN_SCRUB;
-  const bool be = flags & SF_EVAL_BIG_ENDIAN;
-  auto fin = [&](float x, int p) {
-    if (scrub && isnan(x)) x = (p & 1) ? 0.0f : 1.0f;
-    if (be) x = __uint_as_float(__builtin_bswap32(__float_as_uint(x)));
-    return x;
-  };
+    tess_v4f* __restrict__ tab, unsigned flags) {
+  const int DT = D + 1;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= S * DT) return;
+  const int64_t s = e / DT;
+  const int d = (int)(e - s * DT);
+  float v[4];
+  if (d < D) {
+    const int64_t i = s * D + d;
+    double sn, cn;
+    sincos(phase[i], &sn, &cn);
+    const double ax = amp_xx ? amp_xx[i] : 1.0;
+    const double ay = amp_yy ? amp_yy[i] : ax;
+    v[0] = (float)(ax * cn);
+    v[1] = (float)(ax * sn);
+    v[2] = (float)(ay * cn);
+    v[3] = (float)(ay * sn);
+  } else {
+    v[0] = v[1] = v[2] = v[3] = __builtin_nanf("");
+  }
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    if ((flags & SF_EVAL_NAN_SCRUB) && isnan(v[p])) v[p] = (p & 1) ? 0.0f : 1.0f;
+    if (flags & SF_EVAL_BIG_ENDIAN)
+      v[p] = __uint_as_float(__builtin_bswap32(__float_as_uint(v[p])));
+  }
+  tab[e] = tess_v4f{v[0], v[1], v[2], v[3]};
+}
+
+template <int NW, bool VEC4>
+__global__ __launch_bounds__(64 * NW) void kl_tess_gather_kernel(
+    const int32_t* __restrict__ labels, int64_t P,
+    const tess_v4f* __restrict__ tab, int D, int64_t S,
+    float* __restrict__ out, int64_t ring, int64_t ring_base, int64_t n_pb,
+    int64_t n_sc, int chunk) {
+  extern __shared__ tess_v4f gtab[];  // [chunk][D + 1]
+  constexpr int kC = kGatherRun / 256;  // 1 KiB pieces of a wave's run
+  const int DT = D + 1;
+  const int l = threadIdx.x & 63;
+  // wave index, wave-uniform: slot and ring arithmetic stay on the SALU
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   for (int64_t bb = blockIdx.x; bb < n_pb * n_sc; bb += gridDim.x) {
     const int64_t pb = bb % n_pb, sc = bb / n_pb;
-    const int64_t s0 = sc * kGatherSlots;
-    const int ns = (int)((S - s0) < kGatherSlots ? (S - s0) : kGatherSlots);
+    const int64_t s0 = sc * chunk;
+    const int ns = (int)((S - s0) < chunk ? (S - s0) : chunk);
     __syncthreads();  // the previous item's table reads are done
-    for (int e = threadIdx.x; e < ns * DT; e += blockDim.x) {
-      const int k = e / DT, d = e - k * DT;
-      v4f v;
-      if (d < D) {
-        const int64_t i = (s0 + k) * D + d;
-        double sn, cn;
-        sincos(phase[i], &sn, &cn);
-        const double ax = amp_xx ? amp_xx[i] : 1.0;
-        const double ay = amp_yy ? amp_yy[i] : ax;
-        v = v4f{(float)(ax * cn), (float)(ax * sn), (float)(ay * cn), (float)(ay * sn)};
-      } else {
-        const float q = __builtin_nanf("");
-        v = v4f{q, q, q, q};
-      }
-      gtab[e] = v4f{fin(v[0], 0), fin(v[1], 1), fin(v[2], 2), fin(v[3], 3)};
-    }
+    for (int e = threadIdx.x; e < ns * DT; e += blockDim.x) gtab[e] = tab[s0 * DT + e];
     __syncthreads();
-    const int64_t p0 = pb * kGatherRun + 4 * (int64_t)threadIdx.x;
-    if (p0 >= P) continue;  // after the barrier: nothing below syncs
-    int lab[4];
+    // every wave covers the whole run (pixels 256 c + 4 l + j) for its own
+    // slots k = w, w + NW, ...: per (slot, plane) one wave writes
+    // kGatherRun * 4 contiguous bytes
+    const int64_t p0 = pb * kGatherRun + 4 * l;
+    int lab[kC][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int lb = (p0 + j < P) ? labels[p0 + j] - 1 : 0;
-      lab[j] = (lb >= 0 && lb < D) ? lb : D;
-    }
-    for (int k = 0; k < ns; ++k) {
-      const v4f* t = gtab + k * DT;
-      const v4f a = t[lab[0]], b = t[lab[1]], c = t[lab[2]], d = t[lab[3]];
-      float* o = out + ((s0 + k) % ring) * 4 * P + p0;
+    for (int c = 0; c < kC; ++c)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (VEC4) {
-          __builtin_nontemporal_store(v4f{a[q], b[q], c[q], d[q]},
-                                      reinterpret_cast<v4f*>(o + q * P));
-        } else {
-          const float v[4] = {a[q], b[q], c[q], d[q]};
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (p0 + j < P) o[q * P + j] = v[j];
-        }
+      for (int j = 0; j < 4; ++j) {
+        const int64_t p = p0 + 256 * c + j;
+        const int lb = p < P ? labels[p] - 1 : 0;
+        lab[c][j] = (lb >= 0 && lb < D) ? lb : D;
       }
+    for (int k = w; k < ns; k += NW) {
+      const tess_v4f* t = gtab + k * DT;
+      tess_v4f v[kC][4];
+#pragma unroll
+      for (int c = 0; c < kC; ++c)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[c][j] = t[lab[c][j]];
+      // ring slot (ring < 2^31: sf_tess_fill)
+      const int64_t so = (s0 + k + ring_base) % ring;
+      float* o = out + so * 4 * P + p0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int c = 0; c < kC; ++c) {
+          if (VEC4) {
+            if (p0 + 256 * c < P)
+              __builtin_nontemporal_store(
+                  tess_v4f{v[c][0][q], v[c][1][q], v[c][2][q], v[c][3][q]},
+                  reinterpret_cast<tess_v4f*>(o + q * P + 256 * c));
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (p0 + 256 * c + j < P) o[q * P + 256 * c + j] = v[c][j][q];
+          }
+        }
     }
   }
 }
@@ -286,21 +321,56 @@ int launch_tess(sf_ctx* ctx, const int32_t* labels, int nx, int ny,
   if (R == 0) {
     const int64_t P = (int64_t)nx * ny;
     const int64_t n_pb = (P + kGatherRun - 1) / kGatherRun;
-    const int64_t n_sc = (S + kGatherSlots - 1) / kGatherSlots;
-    int64_t grid = n_pb * n_sc;
-    const int64_t cap = ((int64_t)1 << 31) / (64 * kGatherWaves);
-    if (grid > cap) grid = cap;  // workgroups walk the remaining items
-    const size_t lds = (size_t)kGatherSlots * (D + 1) * 4 * sizeof(float);
+    const int64_t DT = D + 1;
+    // the item's table slice in LDS: at most 64 KiB (63 slots at D = 64)
+    int chunk = ctx->tess_slots > 0 ? ctx->tess_slots : kGatherSlotsAuto;
+    if (chunk * DT * 16 > 65536) chunk = (int)(65536 / (DT * 16));
+    // the value table of at most `per` slots at a time (<= 256 MiB of
+    // scratch), a whole number of work-item chunks
+    int64_t per = (((int64_t)256 << 20) / (DT * 16)) / chunk * chunk;
+    if (per < chunk) per = chunk;
+    if (per > S) per = S;
+    const size_t need = (size_t)(per * DT) * 16;
+    if (ctx->tess_tab_cap < need) {
+      if (ctx->d_tess_tab) (void)hipFree(ctx->d_tess_tab);
+      ctx->d_tess_tab = nullptr;
+      ctx->tess_tab_cap = 0;
+      if (hipMalloc(reinterpret_cast<void**>(&ctx->d_tess_tab), need) != hipSuccess) {
+        set_error("sf_tess_fill: hipMalloc of the value table failed");
+        return SF_ENOMEM;
+      }
+      ctx->tess_tab_cap = need;
+    }
+    tess_v4f* tab = reinterpret_cast<tess_v4f*>(ctx->d_tess_tab);
+    const size_t lds = (size_t)chunk * DT * 16;
     const bool vec4 = (P % 4 == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
-    if (vec4)
-      hipLaunchKernelGGL(kl_tess_gather_kernel<true>, dim3((unsigned)grid),
-                         dim3(64 * kGatherWaves), lds, ctx->stream, labels, P,
-                         phase, amp_xx, amp_yy, D, S, out, ring, n_pb, n_sc, flags);
-    else
-      hipLaunchKernelGGL(kl_tess_gather_kernel<false>, dim3((unsigned)grid),
-                         dim3(64 * kGatherWaves), lds, ctx->stream, labels, P,
-                         phase, amp_xx, amp_yy, D, S, out, ring, n_pb, n_sc, flags);
-    SF_HIP(hipGetLastError());
+    for (int64_t b = 0; b < S; b += per) {
+      const int64_t Sb = S - b < per ? S - b : per;
+      const int64_t n_tab = Sb * DT;
+      hipLaunchKernelGGL(kl_tess_table_kernel, dim3((unsigned)((n_tab + 255) / 256)),
+                         dim3(256), 0, ctx->stream, phase + b * D,
+                         amp_xx ? amp_xx + b * D : nullptr,
+                         amp_yy ? amp_yy + b * D : nullptr, D, Sb, tab, flags);
+      SF_HIP(hipGetLastError());
+      const int64_t n_sc = (Sb + chunk - 1) / chunk;
+      int64_t grid = n_pb * n_sc;
+      const int nw = ctx->tess_waves > 0 ? ctx->tess_waves : kGatherWavesAuto;
+      const int64_t cap = ((int64_t)1 << 31) / (64 * nw);
+      if (grid > cap) grid = cap;  // workgroups walk the remaining items
+#define SF_GATHER(NW, V)                                                          \
+  hipLaunchKernelGGL((kl_tess_gather_kernel<NW, V>), dim3((unsigned)grid),       \
+                     dim3(64 * NW), lds, ctx->stream, labels, P, tab, D, Sb, out, \
+                     ring, b % ring, n_pb, n_sc, chunk)
+      if (vec4) {
+        if (nw == 4) SF_GATHER(4, true);
+        else if (nw == 8) SF_GATHER(8, true);
+        else SF_GATHER(16, true);
+      } else {
+        SF_GATHER(4, false);
+      }
+#undef SF_GATHER
+      SF_HIP(hipGetLastError());
+    }
     return SF_OK;
   }
   const int tiles = ((nx + kTT - 1) / kTT) * ((ny + kTT - 1) / kTT);

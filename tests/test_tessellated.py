@@ -276,8 +276,9 @@ def test_tess_rejects_bad_labels():
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,S", [(17, 70), (128, 45), (64, 33), (33, 1)])
 def test_tess_gather_amplitudes_nan_byteswap(n, S):
-    """The unsmoothed gather-store kernel (float4 runs when n^2 % 4 == 0,
-    scalar tail otherwise; slot chunks of 32): gain tables A cos / A sin,
+    """The unsmoothed table + gather-store kernels (float4 runs when
+    n^2 % 4 == 0, scalar tail otherwise; 4 / 8 / 16 waves, slot chunks of
+    3 to 64, ragged last chunks): gain tables A cos / A sin,
     NaN phases and amplitudes (scrubbed to 1 / 0, or left NaN), FITS byte
     order -- vs fp64 numpy cast once to fp32 (<= 1 ulp)."""
     torch = pytest.importorskip("torch")
@@ -301,11 +302,21 @@ def test_tess_gather_amplitudes_nan_byteswap(n, S):
     want = np.moveaxis(tab[:, lab - 1, :], -1, 1)  # [S][4][n][n]
     d = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev)
          for k, v in (("lab", lab), ("ph", ph), ("ax", ax), ("ay", ay))}
-    for flags in (SF_EVAL_NAN_SCRUB, SF_EVAL_NAN_SCRUB | SF_EVAL_BIG_ENDIAN, 0):
+    from ska_sdp_screen_fitting_amd._lib import SF_OPT_TESS_SLOTS, SF_OPT_TESS_WAVES
+    cases = [(fl, 0, 0) for fl in (SF_EVAL_NAN_SCRUB,
+                                   SF_EVAL_NAN_SCRUB | SF_EVAL_BIG_ENDIAN, 0)]
+    cases += [(SF_EVAL_NAN_SCRUB, w, k) for w, k in ((8, 3), (16, 16), (4, 64))]
+    for flags, waves, slots in cases:
         out = torch.full((S, 4, n, n), -5.0, dtype=torch.float32, device=dev)
-        ctx.tess_fill(d["lab"], n, n, d["ph"], D, S, out, amp_xx=d["ax"],
-                      amp_yy=d["ay"], smooth_pix=0.0, flags=flags)
-        torch.cuda.synchronize()
+        ctx.set_option(SF_OPT_TESS_WAVES, waves)
+        ctx.set_option(SF_OPT_TESS_SLOTS, slots)
+        try:
+            ctx.tess_fill(d["lab"], n, n, d["ph"], D, S, out, amp_xx=d["ax"],
+                          amp_yy=d["ay"], smooth_pix=0.0, flags=flags)
+            torch.cuda.synchronize()
+        finally:
+            ctx.set_option(SF_OPT_TESS_WAVES, 0)
+            ctx.set_option(SF_OPT_TESS_SLOTS, 0)
         got = out.cpu().numpy()
         if flags & SF_EVAL_BIG_ENDIAN:
             got = got.byteswap()
