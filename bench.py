@@ -464,7 +464,15 @@ def tess_steps(args, ctx, torch, dev, dist, world, rank, coll_dev, sol, setup,
     if rank == 0:
         bytes_launch = S * (16 * P + 8 * D)
         achieved = bytes_launch / launch_s / 1e9
-        kernel = "kl_tess_gather_kernel" if args.smooth_pix == 0 else "kl_tess_kernel"
+        kernel = ("kl_tess_gather_kernel" if args.smooth_pix == 0
+                  else "kl_tess_smooth_kernel")
+        # PMC traffic (profiles/traffic.json) when measured on this call shape
+        traffic = None
+        tj = _profile_entry("traffic.json", args.workload + "-tess", kernel)
+        if (tj is not None and tj.get("flags") == flags
+                and abs(tj.get("algorithmic_bytes_per_launch", 0) - bytes_launch)
+                <= 1e-6 * bytes_launch):
+            traffic = tj.get("hbm_bytes_per_launch")
         line = {
             "metric": METRIC,
             "value": T * F * (A if args.as_shard_of else A_total) * args.steps / elapsed,
@@ -482,7 +490,7 @@ def tess_steps(args, ctx, torch, dev, dist, world, rank, coll_dev, sol, setup,
                 "parallelism": f"ant-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": None, "kernel": kernel,
+                         "traffic": traffic, "kernel": kernel,
                          "bytes_per_launch": bytes_launch,
                          "launch_ms": launch_s * 1e3},
             "check": {"max_abs_cos2_plus_sin2_minus_1": unit_err,

@@ -156,6 +156,10 @@ int sf_device_cus(sf_ctx* ctx, int* n_cu);
  * identical for every setting. */
 #define SF_OPT_TESS_SLOTS 11
 #define SF_OPT_TESS_WAVES 12
+/* SF_OPT_TESS_TILE = 1 runs sf_tess_fill (radius <= 24) on the round-1 fused
+ * 16 x 16 tile kernel instead of the table + gather / wide-tile smoothing
+ * kernels (same bits; for cross-checks). */
+#define SF_OPT_TESS_TILE 13
 #define SF_EVAL_KERNEL_AUTO 0
 #define SF_EVAL_KERNEL_TILE 1
 #define SF_EVAL_KERNEL_LDS4 2

@@ -198,6 +198,10 @@ int sf_set_option(sf_ctx* ctx, int option, int value) {
                  "sf_set_option: tess slots must be 0..256");
       ctx->tess_slots = value;
       return SF_OK;
+    case SF_OPT_TESS_TILE:
+      SF_REQUIRE(value == 0 || value == 1, SF_EINVAL, "sf_set_option: tess tile must be 0 or 1");
+      ctx->tess_tile = value;
+      return SF_OK;
     case SF_OPT_TESS_WAVES:
       SF_REQUIRE(value == 0 || value == 4 || value == 8 || value == 16, SF_EINVAL,
                  "sf_set_option: tess waves must be 0, 4, 8 or 16");
@@ -503,8 +507,8 @@ int sf_tess_fill(sf_ctx* ctx, const int32_t* labels, int nx, int ny,
   int rc = upload_gaussian(ctx, smooth_pix, &R);
   if (rc != SF_OK) return rc;
   if (R <= sf::kTessMaxR)
-    return sf::launch_tess(ctx, labels, nx, ny, phase, amp_xx, amp_yy, D, S,
-                           out, ring, ctx->d_gw, R, flags);
+    return (ctx->tess_tile ? sf::launch_tess_tile : sf::launch_tess)(
+        ctx, labels, nx, ny, phase, amp_xx, amp_yy, D, S, out, ring, ctx->d_gw, R, flags);
   // wider Gaussians: gather unsmoothed and unscrubbed, then the separable
   // passes of sf_smooth (scrub / byte swap after smoothing, as the
   // reference); every slot needs its own cube for that

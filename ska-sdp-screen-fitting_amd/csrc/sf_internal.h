@@ -99,6 +99,7 @@ struct sf_ctx {
   int eval_bands = 0;           // SF_OPT_EVAL_BANDS (0 = auto = 1)
   int tess_slots = 0;           // SF_OPT_TESS_SLOTS (0 = auto = 16)
   int tess_waves = 0;           // SF_OPT_TESS_WAVES (0 = auto = 16)
+  int tess_tile = 0;            // SF_OPT_TESS_TILE (1: round-1 fused tile kernel)
   int fit_pack = 1;             // SF_OPT_FIT_PACK: 2 slots per wave for D <= 32
   int fit_lean = 1;             // SF_OPT_FIT_LEAN: lean pass when weights are uniform
 };
@@ -128,6 +129,10 @@ int launch_eval(sf_ctx* ctx, const double* coef, const double* cxx,
                 const double* cyy, int64_t S, float* out, int64_t ring,
                 unsigned flags, unsigned* sums);
 int launch_tess(sf_ctx* ctx, const int32_t* labels, int nx, int ny,
+                const double* phase, const double* amp_xx,
+                const double* amp_yy, int D, int64_t S, float* out,
+                int64_t ring, const double* d_w, int R, unsigned flags);
+int launch_tess_tile(sf_ctx* ctx, const int32_t* labels, int nx, int ny,
                 const double* phase, const double* amp_xx,
                 const double* amp_yy, int D, int64_t S, float* out,
                 int64_t ring, const double* d_w, int R, unsigned flags);

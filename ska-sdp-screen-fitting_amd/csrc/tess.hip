@@ -241,6 +241,135 @@ __global__ __launch_bounds__(64 * NW) void kl_tess_gather_kernel(
   }
 }
 
+// Smoothed fill (0 < R <= kMaxR): wide tiles for long store runs.  A
+// workgroup (4 waves) owns a tile of kSmTH rows x kSmTW pixels (wave w:
+// row w, 4 pixels per lane, 1 KiB contiguous per (slot, plane)) and a
+// chunk of slots.  The tile's labels + halo sit in LDS as bytes (D <= 64,
+// entry D = NaN for labels outside 1..D); per slot the raw value table
+// (kl_tess_table_kernel without scrub / swap, widened to double) goes to
+// LDS, the y pass writes the halo columns of the tile rows (fp64 sums in
+// scipy's order -- centre, then the pairs from the outermost in -- rounded
+// to float like scipy's float32 intermediate), the x pass
+// each wave's row, then the NaN scrub and byte swap (the reference scrubs
+// after smoothing).  The same arithmetic in the same order as
+// kl_tess_kernel: the same bits.
+constexpr int kSmTW = 256;
+constexpr int kSmTH = 4;
+constexpr int kSmSlots = 8;
+
+// RT > 0: the radius at compile time (taps unrolled, so the label and table
+// reads of a tap window go out together; LDS sized for RT: more resident
+// workgroups); RT = 0: any R <= kMaxR at run time.
+template <int RT>
+__global__ __launch_bounds__(256) void kl_tess_smooth_kernel(
+    const int32_t* __restrict__ labels, int nx, int ny,
+    const tess_v4f* __restrict__ tab, int D, int64_t S,
+    float* __restrict__ out, int64_t ring, int64_t ring_base,
+    const double* __restrict__ gw, int R_arg, int64_t n_tiles, int64_t n_sc,
+    unsigned flags) {
+#pragma clang fp contract(off)
+  typedef double v4d_t __attribute__((ext_vector_type(4)));
+  constexpr int kR = RT > 0 ? RT : kMaxR;  // LDS sizing
+  const int R = RT > 0 ? RT : R_arg;
+  __shared__ unsigned char lab[(kSmTH + 2 * kR) * (kSmTW + 2 * kR)];
+  // y-pass results: float, as scipy's float32 intermediate image
+  __shared__ tess_v4f ybuf[kSmTH * (kSmTW + 2 * kR)];
+  __shared__ v4d_t tbl[2][65];
+  __shared__ double w[2 * kR + 1];
+  const int DT = D + 1;
+  const int W2 = kSmTW + 2 * R;  // halo tile width
+  const int H2 = kSmTH + 2 * R;
+  const int tiles_x = (nx + kSmTW - 1) / kSmTW;
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const bool scrub = flags & SF_EVAL_NAN_SCRUB;
+  const bool be = flags & SF_EVAL_BIG_ENDIAN;
+  const int64_t P = (int64_t)nx * ny;
+  for (int e = threadIdx.x; e < 2 * R + 1; e += blockDim.x) w[e] = gw[e];
+  for (int64_t bb = blockIdx.x; bb < n_tiles * n_sc; bb += gridDim.x) {
+    const int64_t tile = bb % n_tiles, sc = bb / n_tiles;
+    const int tx0 = (int)(tile % tiles_x) * kSmTW;
+    const int ty0 = (int)(tile / tiles_x) * kSmTH;
+    const int64_t s0 = sc * kSmSlots;
+    const int ns = (int)((S - s0) < kSmSlots ? (S - s0) : kSmSlots);
+    __syncthreads();  // the previous item is done with lab / tbl / ybuf
+    for (int e = threadIdx.x; e < H2 * W2; e += blockDim.x) {
+      const int hy = e / W2, hx = e - hy * W2;
+      const int gy = reflect_idx(ty0 + hy - R, ny);
+      const int gx = reflect_idx(tx0 + hx - R, nx);
+      const int lb = labels[(int64_t)gy * nx + gx] - 1;
+      lab[e] = (unsigned char)((lb >= 0 && lb < D) ? lb : D);
+    }
+    for (int e = threadIdx.x; e < DT; e += blockDim.x) {
+      const tess_v4f v = tab[s0 * DT + e];
+      tbl[0][e] = v4d_t{(double)v[0], (double)v[1], (double)v[2], (double)v[3]};
+    }
+    const int gy = ty0 + wv;  // this wave's output row
+    for (int k = 0; k < ns; ++k) {
+      __syncthreads();  // tbl[k & 1] (and, at k = 0, lab) complete; ybuf free
+      const v4d_t* t = tbl[k & 1];
+      // y pass over the tile rows and every halo column
+      for (int e = threadIdx.x; e < kSmTH * W2; e += blockDim.x) {
+        const int r = e / W2, c = e - r * W2;
+        const unsigned char* col = lab + (r + R) * W2 + c;
+        v4d_t acc = t[col[0]] * w[R];
+#pragma unroll
+        for (int j = R; j >= 1; --j) {
+          const v4d_t a = t[col[-j * W2]], b = t[col[j * W2]];
+          acc += (a + b) * w[R - j];
+        }
+        ybuf[e] = tess_v4f{(float)acc[0], (float)acc[1], (float)acc[2], (float)acc[3]};
+      }
+      // the next slot's table, into the other buffer (its last readers
+      // finished the y pass of slot k - 1 before the barrier above)
+      if (k + 1 < ns)
+        for (int e = threadIdx.x; e < DT; e += blockDim.x) {
+          const tess_v4f v = tab[(s0 + k + 1) * DT + e];
+          tbl[(k + 1) & 1][e] =
+              v4d_t{(double)v[0], (double)v[1], (double)v[2], (double)v[3]};
+        }
+      __syncthreads();
+      // x pass: this wave's row, 4 pixels per lane
+      const int gx0 = tx0 + 4 * l;
+      if (gy >= ny || gx0 >= nx) continue;
+      float v[4][4];  // [pixel][plane]
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const tess_v4f* row = ybuf + wv * W2 + R + 4 * l + i;
+        const tess_v4f c0 = row[0];
+        v4d_t acc = v4d_t{(double)c0[0], (double)c0[1], (double)c0[2], (double)c0[3]} * w[R];
+#pragma unroll
+        for (int j = R; j >= 1; --j) {
+          const tess_v4f a = row[-j], b = row[j];
+          const v4d_t ad = {(double)a[0], (double)a[1], (double)a[2], (double)a[3]};
+          const v4d_t bd = {(double)b[0], (double)b[1], (double)b[2], (double)b[3]};
+          acc += (ad + bd) * w[R - j];
+        }
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          float x = (float)acc[p];
+          if (scrub && isnan(x)) x = (p & 1) ? 0.0f : 1.0f;
+          if (be) x = __uint_as_float(__builtin_bswap32(__float_as_uint(x)));
+          v[i][p] = x;
+        }
+      }
+      const int64_t so = (s0 + k + ring_base) % ring;
+      float* o = out + so * 4 * P + (int64_t)gy * nx + gx0;
+      const bool vec = (nx % 4 == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        if (vec) {
+          __builtin_nontemporal_store(tess_v4f{v[0][p], v[1][p], v[2][p], v[3][p]},
+                                      reinterpret_cast<tess_v4f*>(o + p * P));
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (gx0 + i < nx) o[p * P + i] = v[i][p];
+        }
+      }
+    }
+  }
+}
+
 // Separable Gaussian of Screen.write for any radius (screen.py:353-362:
 // scipy.ndimage.gaussian_filter(img, sigma=(0, s, s)) per (time, freq,
 // station), i.e. per image of the [.][4][ny][nx] cube): one 1-D pass per
@@ -314,65 +443,109 @@ int launch_smooth(sf_ctx* ctx, float* cube, int nx, int ny, int64_t n_img,
   return SF_OK;
 }
 
+// The value table of at most `per` slots (<= 256 MiB of scratch, a multiple
+// of `chunk`) in the context's scratch buffer.
+static int tess_table_alloc(sf_ctx* ctx, int64_t S, int64_t DT, int chunk,
+                            int64_t* per_out) {
+  int64_t per = (((int64_t)256 << 20) / (DT * 16)) / chunk * chunk;
+  if (per < chunk) per = chunk;
+  if (per > S) per = S;
+  const size_t need = (size_t)(per * DT) * 16;
+  if (ctx->tess_tab_cap < need) {
+    if (ctx->d_tess_tab) (void)hipFree(ctx->d_tess_tab);
+    ctx->d_tess_tab = nullptr;
+    ctx->tess_tab_cap = 0;
+    if (hipMalloc(reinterpret_cast<void**>(&ctx->d_tess_tab), need) != hipSuccess) {
+      set_error("sf_tess_fill: hipMalloc of the value table failed");
+      return SF_ENOMEM;
+    }
+    ctx->tess_tab_cap = need;
+  }
+  *per_out = per;
+  return SF_OK;
+}
+
 int launch_tess(sf_ctx* ctx, const int32_t* labels, int nx, int ny,
                 const double* phase, const double* amp_xx,
                 const double* amp_yy, int D, int64_t S, float* out,
                 int64_t ring, const double* d_w, int R, unsigned flags) {
+  const int64_t P = (int64_t)nx * ny;
+  const int64_t DT = D + 1;
+  int chunk = kSmSlots;
   if (R == 0) {
-    const int64_t P = (int64_t)nx * ny;
-    const int64_t n_pb = (P + kGatherRun - 1) / kGatherRun;
-    const int64_t DT = D + 1;
     // the item's table slice in LDS: at most 64 KiB (63 slots at D = 64)
-    int chunk = ctx->tess_slots > 0 ? ctx->tess_slots : kGatherSlotsAuto;
+    chunk = ctx->tess_slots > 0 ? ctx->tess_slots : kGatherSlotsAuto;
     if (chunk * DT * 16 > 65536) chunk = (int)(65536 / (DT * 16));
-    // the value table of at most `per` slots at a time (<= 256 MiB of
-    // scratch), a whole number of work-item chunks
-    int64_t per = (((int64_t)256 << 20) / (DT * 16)) / chunk * chunk;
-    if (per < chunk) per = chunk;
-    if (per > S) per = S;
-    const size_t need = (size_t)(per * DT) * 16;
-    if (ctx->tess_tab_cap < need) {
-      if (ctx->d_tess_tab) (void)hipFree(ctx->d_tess_tab);
-      ctx->d_tess_tab = nullptr;
-      ctx->tess_tab_cap = 0;
-      if (hipMalloc(reinterpret_cast<void**>(&ctx->d_tess_tab), need) != hipSuccess) {
-        set_error("sf_tess_fill: hipMalloc of the value table failed");
-        return SF_ENOMEM;
+  }
+  int64_t per = 0;
+  const int rc = tess_table_alloc(ctx, S, DT, chunk, &per);
+  if (rc != SF_OK) return rc;
+  tess_v4f* tab = reinterpret_cast<tess_v4f*>(ctx->d_tess_tab);
+  // unsmoothed, the table entries are the pixels: scrub / swap them there
+  const unsigned tab_flags = R == 0 ? flags : 0u;
+  for (int64_t b = 0; b < S; b += per) {
+    const int64_t Sb = S - b < per ? S - b : per;
+    const int64_t n_tab = Sb * DT;
+    hipLaunchKernelGGL(kl_tess_table_kernel, dim3((unsigned)((n_tab + 255) / 256)),
+                       dim3(256), 0, ctx->stream, phase + b * D,
+                       amp_xx ? amp_xx + b * D : nullptr,
+                       amp_yy ? amp_yy + b * D : nullptr, D, Sb, tab, tab_flags);
+    SF_HIP(hipGetLastError());
+    const int64_t n_sc = (Sb + chunk - 1) / chunk;
+    if (R > 0) {
+      const int64_t n_tiles = (int64_t)((nx + kSmTW - 1) / kSmTW) * ((ny + kSmTH - 1) / kSmTH);
+      int64_t grid = n_tiles * n_sc;
+      const int64_t cap = ((int64_t)1 << 31) / 256;
+      if (grid > cap) grid = cap;  // workgroups walk the remaining items
+#define SF_SMOOTH(RT)                                                             \
+  hipLaunchKernelGGL(kl_tess_smooth_kernel<RT>, dim3((unsigned)grid), dim3(256), 0, \
+                     ctx->stream, labels, nx, ny, tab, D, Sb, out, ring, b % ring,  \
+                     d_w, R, n_tiles, n_sc, flags)
+      switch (R) {
+        case 1: SF_SMOOTH(1); break;
+        case 2: SF_SMOOTH(2); break;
+        case 3: SF_SMOOTH(3); break;
+        case 4: SF_SMOOTH(4); break;
+        case 5: SF_SMOOTH(5); break;
+        case 6: SF_SMOOTH(6); break;
+        case 7: SF_SMOOTH(7); break;
+        case 8: SF_SMOOTH(8); break;
+        default: SF_SMOOTH(0);
       }
-      ctx->tess_tab_cap = need;
+#undef SF_SMOOTH
+      SF_HIP(hipGetLastError());
+      continue;
     }
-    tess_v4f* tab = reinterpret_cast<tess_v4f*>(ctx->d_tess_tab);
+    const int64_t n_pb = (P + kGatherRun - 1) / kGatherRun;
     const size_t lds = (size_t)chunk * DT * 16;
     const bool vec4 = (P % 4 == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
-    for (int64_t b = 0; b < S; b += per) {
-      const int64_t Sb = S - b < per ? S - b : per;
-      const int64_t n_tab = Sb * DT;
-      hipLaunchKernelGGL(kl_tess_table_kernel, dim3((unsigned)((n_tab + 255) / 256)),
-                         dim3(256), 0, ctx->stream, phase + b * D,
-                         amp_xx ? amp_xx + b * D : nullptr,
-                         amp_yy ? amp_yy + b * D : nullptr, D, Sb, tab, flags);
-      SF_HIP(hipGetLastError());
-      const int64_t n_sc = (Sb + chunk - 1) / chunk;
-      int64_t grid = n_pb * n_sc;
-      const int nw = ctx->tess_waves > 0 ? ctx->tess_waves : kGatherWavesAuto;
-      const int64_t cap = ((int64_t)1 << 31) / (64 * nw);
-      if (grid > cap) grid = cap;  // workgroups walk the remaining items
+    int64_t grid = n_pb * n_sc;
+    const int nw = ctx->tess_waves > 0 ? ctx->tess_waves : kGatherWavesAuto;
+    const int64_t cap = ((int64_t)1 << 31) / (64 * nw);
+    if (grid > cap) grid = cap;  // workgroups walk the remaining items
 #define SF_GATHER(NW, V)                                                          \
   hipLaunchKernelGGL((kl_tess_gather_kernel<NW, V>), dim3((unsigned)grid),       \
                      dim3(64 * NW), lds, ctx->stream, labels, P, tab, D, Sb, out, \
                      ring, b % ring, n_pb, n_sc, chunk)
-      if (vec4) {
-        if (nw == 4) SF_GATHER(4, true);
-        else if (nw == 8) SF_GATHER(8, true);
-        else SF_GATHER(16, true);
-      } else {
-        SF_GATHER(4, false);
-      }
-#undef SF_GATHER
-      SF_HIP(hipGetLastError());
+    if (vec4) {
+      if (nw == 4) SF_GATHER(4, true);
+      else if (nw == 8) SF_GATHER(8, true);
+      else SF_GATHER(16, true);
+    } else {
+      SF_GATHER(4, false);
     }
-    return SF_OK;
+#undef SF_GATHER
+    SF_HIP(hipGetLastError());
   }
+  return SF_OK;
+}
+
+// The round-1 fused tile kernel (16 x 16 tiles, table built per tile), kept
+// for cross-checks (SF_OPT_TESS_TILE): same bits as launch_tess.
+int launch_tess_tile(sf_ctx* ctx, const int32_t* labels, int nx, int ny,
+                     const double* phase, const double* amp_xx,
+                     const double* amp_yy, int D, int64_t S, float* out,
+                     int64_t ring, const double* d_w, int R, unsigned flags) {
   const int tiles = ((nx + kTT - 1) / kTT) * ((ny + kTT - 1) / kTT);
   const int64_t chunks = (S + kTessSlots - 1) / kTessSlots;
   hipLaunchKernelGGL(kl_tess_kernel, dim3(tiles, (unsigned)chunks), dim3(256),

@@ -33,6 +33,7 @@ SF_OPT_EVAL_BANDS = 9
 SF_OPT_FIT_LEAN = 10
 SF_OPT_TESS_SLOTS = 11
 SF_OPT_TESS_WAVES = 12
+SF_OPT_TESS_TILE = 13
 SF_EVAL_KERNEL_AUTO = 0
 SF_EVAL_KERNEL_TILE = 1
 SF_EVAL_KERNEL_LDS4 = 2

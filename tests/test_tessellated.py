@@ -327,3 +327,45 @@ def test_tess_gather_amplitudes_nan_byteswap(n, S):
             assert not nan.any()
         diff = np.abs(got.view(np.int32).astype(np.int64) - exp.view(np.int32))
         assert diff[~nan].max() <= 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nx,ny,sigma", [(17, 17, 0.5), (53, 37, 1.3), (128, 128, 0.0),
+                                         (300, 260, 4.0), (64, 64, 6.0), (20, 9, 0.3)])
+def test_tess_kernels_agree_with_tile_kernel(nx, ny, sigma):
+    """The table + gather (R = 0) and wide-tile smoothing (R <= 24) kernels
+    write the same bits as the round-1 fused 16 x 16 tile kernel
+    (SF_OPT_TESS_TILE): ragged tiles and slot chunks, NaN phases and
+    amplitudes, labels of every cell, scrub / byte-swap flags."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from ska_sdp_screen_fitting_amd import get_context
+    from ska_sdp_screen_fitting_amd._lib import (SF_EVAL_BIG_ENDIAN, SF_EVAL_NAN_SCRUB,
+                                                 SF_OPT_TESS_TILE)
+    dev = torch.device("cuda", 0)
+    ctx = get_context(0)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    rng = np.random.default_rng(nx * 7 + ny)
+    D, S = 11, 21
+    lab = rng.integers(1, D + 1, size=(ny, nx)).astype(np.int32)
+    lab[: ny // 2, : nx // 2] = 3  # a constant region too
+    ph = rng.uniform(-9.0, 9.0, size=(S, D))
+    ph[4, 3] = np.nan
+    ax = 10.0 ** rng.normal(0.0, 0.3, size=(S, D))
+    ax[S - 1, 2] = np.nan
+    t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev)
+         for k, v in (("lab", lab), ("ph", ph), ("ax", ax))}
+    for flags in (SF_EVAL_NAN_SCRUB, SF_EVAL_NAN_SCRUB | SF_EVAL_BIG_ENDIAN, 0):
+        res = []
+        for tile in (0, 1):
+            out = torch.full((S, 4, ny, nx), -5.0, dtype=torch.float32, device=dev)
+            ctx.set_option(SF_OPT_TESS_TILE, tile)
+            try:
+                ctx.tess_fill(t["lab"], nx, ny, t["ph"], D, S, out, amp_xx=t["ax"],
+                              smooth_pix=sigma, flags=flags)
+                torch.cuda.synchronize()
+            finally:
+                ctx.set_option(SF_OPT_TESS_TILE, 0)
+            res.append(out.cpu().numpy().view(np.uint32))
+        assert np.array_equal(res[0], res[1]), (flags, int((res[0] != res[1]).sum()))
