@@ -260,7 +260,7 @@ constexpr int kSmSlots = 8;
 // RT > 0: the radius at compile time (taps unrolled, so the label and table
 // reads of a tap window go out together; LDS sized for RT: more resident
 // workgroups); RT = 0: any R <= kMaxR at run time.
-template <int RT>
+template <int RT, int NP>
 __global__ __launch_bounds__(256) void kl_tess_smooth_kernel(
     const int32_t* __restrict__ labels, int nx, int ny,
     const tess_v4f* __restrict__ tab, int D, int64_t S,
@@ -268,13 +268,25 @@ __global__ __launch_bounds__(256) void kl_tess_smooth_kernel(
     const double* __restrict__ gw, int R_arg, int64_t n_tiles, int64_t n_sc,
     unsigned flags) {
 #pragma clang fp contract(off)
-  typedef double v4d_t __attribute__((ext_vector_type(4)));
+  // NP = 2: planes 2 / 3 repeat planes 0 / 1 (no YY amplitude: A_yy = A_xx),
+  // so only two planes are smoothed and each is stored twice
+  typedef double vacc_t __attribute__((ext_vector_type(NP)));
+  typedef float vyf_t __attribute__((ext_vector_type(NP)));
+  auto widen = [](const auto& v) {
+    vacc_t r;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) r[p] = (double)v[p];
+    return r;
+  };
   constexpr int kR = RT > 0 ? RT : kMaxR;  // LDS sizing
   const int R = RT > 0 ? RT : R_arg;
+  // RT > 0: every tap unrolled; a run-time R: 4 taps per trip, so the label
+  // and table reads of 4 taps go out together
+  constexpr int kTapUnroll = RT > 0 ? RT : 4;
   __shared__ unsigned char lab[(kSmTH + 2 * kR) * (kSmTW + 2 * kR)];
   // y-pass results: float, as scipy's float32 intermediate image
-  __shared__ tess_v4f ybuf[kSmTH * (kSmTW + 2 * kR)];
-  __shared__ v4d_t tbl[2][65];
+  __shared__ vyf_t ybuf[kSmTH * (kSmTW + 2 * kR)];
+  __shared__ vacc_t tbl[2][65];
   __shared__ double w[2 * kR + 1];
   const int DT = D + 1;
   const int W2 = kSmTW + 2 * R;  // halo tile width
@@ -300,32 +312,32 @@ __global__ __launch_bounds__(256) void kl_tess_smooth_kernel(
       lab[e] = (unsigned char)((lb >= 0 && lb < D) ? lb : D);
     }
     for (int e = threadIdx.x; e < DT; e += blockDim.x) {
-      const tess_v4f v = tab[s0 * DT + e];
-      tbl[0][e] = v4d_t{(double)v[0], (double)v[1], (double)v[2], (double)v[3]};
+      tbl[0][e] = widen(tab[s0 * DT + e]);
     }
     const int gy = ty0 + wv;  // this wave's output row
     for (int k = 0; k < ns; ++k) {
       __syncthreads();  // tbl[k & 1] (and, at k = 0, lab) complete; ybuf free
-      const v4d_t* t = tbl[k & 1];
+      const vacc_t* t = tbl[k & 1];
       // y pass over the tile rows and every halo column
       for (int e = threadIdx.x; e < kSmTH * W2; e += blockDim.x) {
         const int r = e / W2, c = e - r * W2;
         const unsigned char* col = lab + (r + R) * W2 + c;
-        v4d_t acc = t[col[0]] * w[R];
-#pragma unroll
+        vacc_t acc = t[col[0]] * w[R];
+#pragma unroll kTapUnroll
         for (int j = R; j >= 1; --j) {
-          const v4d_t a = t[col[-j * W2]], b = t[col[j * W2]];
+          const vacc_t a = t[col[-j * W2]], b = t[col[j * W2]];
           acc += (a + b) * w[R - j];
         }
-        ybuf[e] = tess_v4f{(float)acc[0], (float)acc[1], (float)acc[2], (float)acc[3]};
+        vyf_t y;
+#pragma unroll
+        for (int p = 0; p < NP; ++p) y[p] = (float)acc[p];
+        ybuf[e] = y;
       }
       // the next slot's table, into the other buffer (its last readers
       // finished the y pass of slot k - 1 before the barrier above)
       if (k + 1 < ns)
         for (int e = threadIdx.x; e < DT; e += blockDim.x) {
-          const tess_v4f v = tab[(s0 + k + 1) * DT + e];
-          tbl[(k + 1) & 1][e] =
-              v4d_t{(double)v[0], (double)v[1], (double)v[2], (double)v[3]};
+          tbl[(k + 1) & 1][e] = widen(tab[(s0 + k + 1) * DT + e]);
         }
       __syncthreads();
       // x pass: this wave's row, 4 pixels per lane
@@ -334,19 +346,15 @@ __global__ __launch_bounds__(256) void kl_tess_smooth_kernel(
       float v[4][4];  // [pixel][plane]
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const tess_v4f* row = ybuf + wv * W2 + R + 4 * l + i;
-        const tess_v4f c0 = row[0];
-        v4d_t acc = v4d_t{(double)c0[0], (double)c0[1], (double)c0[2], (double)c0[3]} * w[R];
-#pragma unroll
+        const vyf_t* row = ybuf + wv * W2 + R + 4 * l + i;
+        vacc_t acc = widen(row[0]) * w[R];
+#pragma unroll kTapUnroll
         for (int j = R; j >= 1; --j) {
-          const tess_v4f a = row[-j], b = row[j];
-          const v4d_t ad = {(double)a[0], (double)a[1], (double)a[2], (double)a[3]};
-          const v4d_t bd = {(double)b[0], (double)b[1], (double)b[2], (double)b[3]};
-          acc += (ad + bd) * w[R - j];
+          acc += (widen(row[-j]) + widen(row[j])) * w[R - j];
         }
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
-          float x = (float)acc[p];
+          float x = (float)acc[p % NP];
           if (scrub && isnan(x)) x = (p & 1) ? 0.0f : 1.0f;
           if (be) x = __uint_as_float(__builtin_bswap32(__float_as_uint(x)));
           v[i][p] = x;
@@ -497,10 +505,17 @@ int launch_tess(sf_ctx* ctx, const int32_t* labels, int nx, int ny,
       int64_t grid = n_tiles * n_sc;
       const int64_t cap = ((int64_t)1 << 31) / 256;
       if (grid > cap) grid = cap;  // workgroups walk the remaining items
-#define SF_SMOOTH(RT)                                                             \
-  hipLaunchKernelGGL(kl_tess_smooth_kernel<RT>, dim3((unsigned)grid), dim3(256), 0, \
-                     ctx->stream, labels, nx, ny, tab, D, Sb, out, ring, b % ring,  \
-                     d_w, R, n_tiles, n_sc, flags)
+#define SF_SMOOTH(RT)                                                               \
+  do {                                                                              \
+    if (amp_yy)                                                                     \
+      hipLaunchKernelGGL((kl_tess_smooth_kernel<RT, 4>), dim3((unsigned)grid),      \
+                         dim3(256), 0, ctx->stream, labels, nx, ny, tab, D, Sb, out, \
+                         ring, b % ring, d_w, R, n_tiles, n_sc, flags);             \
+    else                                                                            \
+      hipLaunchKernelGGL((kl_tess_smooth_kernel<RT, 2>), dim3((unsigned)grid),      \
+                         dim3(256), 0, ctx->stream, labels, nx, ny, tab, D, Sb, out, \
+                         ring, b % ring, d_w, R, n_tiles, n_sc, flags);             \
+  } while (0)
       switch (R) {
         case 1: SF_SMOOTH(1); break;
         case 2: SF_SMOOTH(2); break;

@@ -354,18 +354,22 @@ def test_tess_kernels_agree_with_tile_kernel(nx, ny, sigma):
     ph[4, 3] = np.nan
     ax = 10.0 ** rng.normal(0.0, 0.3, size=(S, D))
     ax[S - 1, 2] = np.nan
+    ay = 10.0 ** rng.normal(0.0, 0.3, size=(S, D))
     t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev)
-         for k, v in (("lab", lab), ("ph", ph), ("ax", ax))}
-    for flags in (SF_EVAL_NAN_SCRUB, SF_EVAL_NAN_SCRUB | SF_EVAL_BIG_ENDIAN, 0):
+         for k, v in (("lab", lab), ("ph", ph), ("ax", ax), ("ay", ay))}
+    # without a YY amplitude planes 2 / 3 repeat 0 / 1 (smoothed once)
+    for flags, yy in ((SF_EVAL_NAN_SCRUB, None), (SF_EVAL_NAN_SCRUB | SF_EVAL_BIG_ENDIAN, None),
+                      (0, None), (SF_EVAL_NAN_SCRUB, t["ay"]), (0, t["ay"])):
         res = []
         for tile in (0, 1):
             out = torch.full((S, 4, ny, nx), -5.0, dtype=torch.float32, device=dev)
             ctx.set_option(SF_OPT_TESS_TILE, tile)
             try:
                 ctx.tess_fill(t["lab"], nx, ny, t["ph"], D, S, out, amp_xx=t["ax"],
-                              smooth_pix=sigma, flags=flags)
+                              amp_yy=yy, smooth_pix=sigma, flags=flags)
                 torch.cuda.synchronize()
             finally:
                 ctx.set_option(SF_OPT_TESS_TILE, 0)
             res.append(out.cpu().numpy().view(np.uint32))
-        assert np.array_equal(res[0], res[1]), (flags, int((res[0] != res[1]).sum()))
+        assert np.array_equal(res[0], res[1]), (flags, yy is None,
+                                                int((res[0] != res[1]).sum()))
