@@ -318,7 +318,28 @@ __global__ __launch_bounds__(256) void kl_tess_smooth_kernel(
     for (int k = 0; k < ns; ++k) {
       __syncthreads();  // tbl[k & 1] (and, at k = 0, lab) complete; ybuf free
       const vacc_t* t = tbl[k & 1];
-      // y pass over the tile rows and every halo column
+      // y pass over the tile rows and every halo column; compile-time R: a
+      // thread takes whole columns and slides the kSmTH + 2R window of
+      // table values (read once) down its kSmTH rows
+      if constexpr (RT > 0) {
+        constexpr int HW = kSmTH + 2 * RT;
+        for (int c = threadIdx.x; c < W2; c += blockDim.x) {
+          vacc_t win[HW];
+#pragma unroll
+          for (int h = 0; h < HW; ++h) win[h] = t[lab[h * W2 + c]];
+#pragma unroll
+          for (int r = 0; r < kSmTH; ++r) {
+            vacc_t acc = win[r + RT] * w[RT];
+#pragma unroll
+            for (int j = RT; j >= 1; --j)
+              acc += (win[r + RT - j] + win[r + RT + j]) * w[RT - j];
+            vyf_t y;
+#pragma unroll
+            for (int p = 0; p < NP; ++p) y[p] = (float)acc[p];
+            ybuf[r * W2 + c] = y;
+          }
+        }
+      } else
       for (int e = threadIdx.x; e < kSmTH * W2; e += blockDim.x) {
         const int r = e / W2, c = e - r * W2;
         const unsigned char* col = lab + (r + R) * W2 + c;
@@ -344,13 +365,29 @@ __global__ __launch_bounds__(256) void kl_tess_smooth_kernel(
       const int gx0 = tx0 + 4 * l;
       if (gy >= ny || gx0 >= nx) continue;
       float v[4][4];  // [pixel][plane]
+      // compile-time R: the lane's 4 pixels share one 4 + 2R window
+      constexpr int XW = RT > 0 ? 4 + 2 * RT : 1;
+      vacc_t xwin[XW];
+      if constexpr (RT > 0) {
+        const vyf_t* base = ybuf + wv * W2 + 4 * l;
+#pragma unroll
+        for (int h = 0; h < XW; ++h) xwin[h] = widen(base[h]);
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const vyf_t* row = ybuf + wv * W2 + R + 4 * l + i;
-        vacc_t acc = widen(row[0]) * w[R];
+        vacc_t acc;
+        if constexpr (RT > 0) {
+          acc = xwin[RT + i] * w[RT];
+#pragma unroll
+          for (int j = RT; j >= 1; --j)
+            acc += (xwin[RT + i - j] + xwin[RT + i + j]) * w[RT - j];
+        } else {
+          const vyf_t* row = ybuf + wv * W2 + R + 4 * l + i;
+          acc = widen(row[0]) * w[R];
 #pragma unroll kTapUnroll
-        for (int j = R; j >= 1; --j) {
-          acc += (widen(row[-j]) + widen(row[j])) * w[R - j];
+          for (int j = R; j >= 1; --j) {
+            acc += (widen(row[-j]) + widen(row[j])) * w[R - j];
+          }
         }
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
