@@ -243,7 +243,7 @@ __global__ __launch_bounds__(64 * NW) void kl_tess_gather_kernel(
 
 // Smoothed fill (0 < R <= kMaxR): wide tiles for long store runs.  A
 // workgroup (4 waves) owns a tile of kSmTH rows x kSmTW pixels (wave w:
-// row w, 4 pixels per lane, 1 KiB contiguous per (slot, plane)) and a
+// rows w, w + 4, 4 pixels per lane, 1 KiB contiguous per (slot, plane)) and a
 // chunk of slots.  The tile's labels + halo sit in LDS as bytes (D <= 64,
 // entry D = NaN for labels outside 1..D); per slot the raw value table
 // (kl_tess_table_kernel without scrub / swap, widened to double) goes to
@@ -254,7 +254,10 @@ __global__ __launch_bounds__(64 * NW) void kl_tess_gather_kernel(
 // after smoothing).  The same arithmetic in the same order as
 // kl_tess_kernel: the same bits.
 constexpr int kSmTW = 256;
-constexpr int kSmTH = 4;
+// tile rows by radius: 4 for R <= 2 (0.5 px: 18.1 vs 20.1 ms with 8), 8 above
+// (more rows per y-pass window: 1.3 / 2 px 26.4 / 38.4 -> 25.1 / 36.2 ms;
+// profiles/round2zi_tess_smooth_rows.txt)
+__host__ __device__ constexpr int smooth_rows(int R) { return (R >= 1 && R <= 2) ? 4 : 8; }
 constexpr int kSmSlots = 8;
 
 // RT > 0: the radius at compile time (taps unrolled, so the label and table
@@ -279,6 +282,7 @@ __global__ __launch_bounds__(256) void kl_tess_smooth_kernel(
     return r;
   };
   constexpr int kR = RT > 0 ? RT : kMaxR;  // LDS sizing
+  constexpr int kSmTH = smooth_rows(RT);
   const int R = RT > 0 ? RT : R_arg;
   // RT > 0: every tap unrolled; a run-time R: 4 taps per trip, so the label
   // and table reads of 4 taps go out together
@@ -314,7 +318,6 @@ __global__ __launch_bounds__(256) void kl_tess_smooth_kernel(
     for (int e = threadIdx.x; e < DT; e += blockDim.x) {
       tbl[0][e] = widen(tab[s0 * DT + e]);
     }
-    const int gy = ty0 + wv;  // this wave's output row
     for (int k = 0; k < ns; ++k) {
       __syncthreads();  // tbl[k & 1] (and, at k = 0, lab) complete; ybuf free
       const vacc_t* t = tbl[k & 1];
@@ -361,15 +364,17 @@ __global__ __launch_bounds__(256) void kl_tess_smooth_kernel(
           tbl[(k + 1) & 1][e] = widen(tab[(s0 + k + 1) * DT + e]);
         }
       __syncthreads();
-      // x pass: this wave's row, 4 pixels per lane
+      // x pass: wave w takes rows w, w + 4, ...; 4 pixels per lane
       const int gx0 = tx0 + 4 * l;
+      for (int rr = wv; rr < kSmTH; rr += 4) {
+      const int gy = ty0 + rr;
       if (gy >= ny || gx0 >= nx) continue;
       float v[4][4];  // [pixel][plane]
       // compile-time R: the lane's 4 pixels share one 4 + 2R window
       constexpr int XW = RT > 0 ? 4 + 2 * RT : 1;
       vacc_t xwin[XW];
       if constexpr (RT > 0) {
-        const vyf_t* base = ybuf + wv * W2 + 4 * l;
+        const vyf_t* base = ybuf + rr * W2 + 4 * l;
 #pragma unroll
         for (int h = 0; h < XW; ++h) xwin[h] = widen(base[h]);
       }
@@ -382,7 +387,7 @@ __global__ __launch_bounds__(256) void kl_tess_smooth_kernel(
           for (int j = RT; j >= 1; --j)
             acc += (xwin[RT + i - j] + xwin[RT + i + j]) * w[RT - j];
         } else {
-          const vyf_t* row = ybuf + wv * W2 + R + 4 * l + i;
+          const vyf_t* row = ybuf + rr * W2 + R + 4 * l + i;
           acc = widen(row[0]) * w[R];
 #pragma unroll kTapUnroll
           for (int j = R; j >= 1; --j) {
@@ -411,6 +416,7 @@ __global__ __launch_bounds__(256) void kl_tess_smooth_kernel(
             if (gx0 + i < nx) o[p * P + i] = v[i][p];
         }
       }
+      }  // rows of this wave
     }
   }
 }
@@ -538,7 +544,8 @@ int launch_tess(sf_ctx* ctx, const int32_t* labels, int nx, int ny,
     SF_HIP(hipGetLastError());
     const int64_t n_sc = (Sb + chunk - 1) / chunk;
     if (R > 0) {
-      const int64_t n_tiles = (int64_t)((nx + kSmTW - 1) / kSmTW) * ((ny + kSmTH - 1) / kSmTH);
+      const int rows = smooth_rows(R <= 8 ? R : 0);  // the kernel's kSmTH
+      const int64_t n_tiles = (int64_t)((nx + kSmTW - 1) / kSmTW) * ((ny + rows - 1) / rows);
       int64_t grid = n_tiles * n_sc;
       const int64_t cap = ((int64_t)1 << 31) / 256;
       if (grid > cap) grid = cap;  // workgroups walk the remaining items
