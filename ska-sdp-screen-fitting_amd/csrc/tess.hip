@@ -7,9 +7,12 @@
 //     {A_xx cos(phi), A_xx sin(phi), A_yy cos(phi), A_yy sin(phi)}
 // with g = identity or the separable Gaussian (axis y then axis x, float32
 // between the passes, 'reflect' borders, scipy's symmetric-kernel summation
-// order in float64).  One workgroup = a 16 x 16 output tile and a chunk of
-// slots; the label tile (+halo) stays in LDS for the whole chunk, so the only
-// HBM traffic is the 16 B / pixel / slot output write.
+// order in float64).  sf_tess_fill runs a per-slot value-table pass and then
+// kl_tess_gather_kernel (no smoothing) or kl_tess_smooth_kernel (radius <=
+// kMaxR), both below; kl_tess_kernel, the round-1 fused kernel (one
+// workgroup = a 16 x 16 output tile and a chunk of slots, label tile + halo
+// in LDS), stays for cross-checks (SF_OPT_TESS_TILE).  In every variant the
+// only large HBM traffic is the 16 B / pixel / slot output write.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -426,7 +429,7 @@ __global__ __launch_bounds__(256) void kl_tess_smooth_kernel(
 // station), i.e. per image of the [.][4][ny][nx] cube): one 1-D pass per
 // launch, axis y then axis x, float64 sums in scipy's order (centre first,
 // then the symmetric pairs from the outermost in), float32 between the
-// passes, 'reflect' borders.  The fused LDS tile of kl_tess_kernel covers
+// passes, 'reflect' borders.  The LDS tiles of kl_tess_smooth_kernel cover
 // R <= kMaxR; this pair of kernels (one thread per output pixel, neighbours
 // from L1 / L2) covers every R, with the NaN scrub and byte swap of the cube
 // after the second pass (the reference scrubs after smoothing).

@@ -8,7 +8,9 @@ with rounded vertices, then an exact border test of the outline pixels,
 quirk Q10) and a nearest-label fallback for uncovered pixels.  The per-slot
 work -- gather of each direction's (amplitude x) cos / sin into its cells and
 the optional Gaussian smoothing of ``Screen.write`` (screen.py:353-362) --
-runs in the HIP kernel ``kl_tess_kernel`` through ``sf_tess_fill``.
+runs on the GPU through ``sf_tess_fill``: a per-slot value-table kernel, then
+the gather-store kernel (no smoothing) or the wide-tile smoothing kernel
+(csrc/tess.hip).
 """
 
 import os
