@@ -468,7 +468,8 @@ def tess_steps(args, ctx, torch, dev, dist, world, rank, coll_dev, sol, setup,
                   else "kl_tess_smooth_kernel")
         # PMC traffic (profiles/traffic.json) when measured on this call shape
         traffic = None
-        tj = _profile_entry("traffic.json", args.workload + "-tess", kernel)
+        wkey = args.workload + "-tess" + (f"-s{args.smooth_pix:g}" if args.smooth_pix else "")
+        tj = _profile_entry("traffic.json", wkey, kernel)
         if (tj is not None and tj.get("flags") == flags
                 and abs(tj.get("algorithmic_bytes_per_launch", 0) - bytes_launch)
                 <= 1e-6 * bytes_launch):
