@@ -324,17 +324,22 @@ __global__ __launch_bounds__(256) void kl_tess_smooth_kernel(
     for (int k = 0; k < ns; ++k) {
       __syncthreads();  // tbl[k & 1] (and, at k = 0, lab) complete; ybuf free
       const vacc_t* t = tbl[k & 1];
-      // y pass over the tile rows and every halo column; compile-time R: a
-      // thread takes whole columns and slides the kSmTH + 2R window of
-      // table values (read once) down its kSmTH rows
+      // y pass over the tile rows and every halo column; compile-time R: an
+      // item = (column, half of the tile rows): it slides one kYR + 2R
+      // window of table values (read once) down its kYR rows; half-height
+      // items split the W2 > 256 columns' tail trip in two
       if constexpr (RT > 0) {
-        constexpr int HW = kSmTH + 2 * RT;
-        for (int c = threadIdx.x; c < W2; c += blockDim.x) {
+        constexpr int kYR = kSmTH / 2;
+        constexpr int HW = kYR + 2 * RT;
+        for (int e = threadIdx.x; e < 2 * W2; e += blockDim.x) {
+          const int g = e >= W2;
+          const int c = e - g * W2;
+          const int r0 = g * kYR;
           vacc_t win[HW];
 #pragma unroll
-          for (int h = 0; h < HW; ++h) win[h] = t[lab[h * W2 + c]];
+          for (int h = 0; h < HW; ++h) win[h] = t[lab[(r0 + h) * W2 + c]];
 #pragma unroll
-          for (int r = 0; r < kSmTH; ++r) {
+          for (int r = 0; r < kYR; ++r) {
             vacc_t acc = win[r + RT] * w[RT];
 #pragma unroll
             for (int j = RT; j >= 1; --j)
@@ -342,7 +347,7 @@ __global__ __launch_bounds__(256) void kl_tess_smooth_kernel(
             vyf_t y;
 #pragma unroll
             for (int p = 0; p < NP; ++p) y[p] = (float)acc[p];
-            ybuf[r * W2 + c] = y;
+            ybuf[(r0 + r) * W2 + c] = y;
           }
         }
       } else
