@@ -552,7 +552,7 @@ int launch_tess(sf_ctx* ctx, const int32_t* labels, int nx, int ny,
     SF_HIP(hipGetLastError());
     const int64_t n_sc = (Sb + chunk - 1) / chunk;
     if (R > 0) {
-      const int rows = smooth_rows(R <= 8 ? R : 0);  // the kernel's kSmTH
+      const int rows = smooth_rows(R);  // the kernel's kSmTH (8 for every R > 2)
       const int64_t n_tiles = (int64_t)((nx + kSmTW - 1) / kSmTW) * ((ny + rows - 1) / rows);
       int64_t grid = n_tiles * n_sc;
       const int64_t cap = ((int64_t)1 << 31) / 256;
@@ -568,6 +568,10 @@ int launch_tess(sf_ctx* ctx, const int32_t* labels, int nx, int ny,
                          dim3(256), 0, ctx->stream, labels, nx, ny, tab, D, Sb, out, \
                          ring, b % ring, d_w, R, n_tiles, n_sc, flags);             \
   } while (0)
+#define SF_SMOOTH2(RT)                                                              \
+  hipLaunchKernelGGL((kl_tess_smooth_kernel<RT, 2>), dim3((unsigned)grid), dim3(256), \
+                     0, ctx->stream, labels, nx, ny, tab, D, Sb, out, ring, b % ring,  \
+                     d_w, R, n_tiles, n_sc, flags)
       switch (R) {
         case 1: SF_SMOOTH(1); break;
         case 2: SF_SMOOTH(2); break;
@@ -577,9 +581,19 @@ int launch_tess(sf_ctx* ctx, const int32_t* labels, int nx, int ny,
         case 6: SF_SMOOTH(6); break;
         case 7: SF_SMOOTH(7); break;
         case 8: SF_SMOOTH(8); break;
+        // R = 12 / 16 compiled for two planes only (four would spill)
+        case 12:
+        case 16:
+          if (!amp_yy) {
+            if (R == 12) SF_SMOOTH2(12); else SF_SMOOTH2(16);
+            break;
+          }
+          SF_SMOOTH(0);
+          break;
         default: SF_SMOOTH(0);
       }
 #undef SF_SMOOTH
+#undef SF_SMOOTH2
       SF_HIP(hipGetLastError());
       continue;
     }
