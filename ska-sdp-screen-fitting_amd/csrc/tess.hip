@@ -581,15 +581,24 @@ int launch_tess(sf_ctx* ctx, const int32_t* labels, int nx, int ny,
         case 6: SF_SMOOTH(6); break;
         case 7: SF_SMOOTH(7); break;
         case 8: SF_SMOOTH(8); break;
-        // R = 12 / 16 compiled for two planes only (four would spill)
-        case 12:
-        case 16:
-          if (!amp_yy) {
-            if (R == 12) SF_SMOOTH2(12); else SF_SMOOTH2(16);
-            break;
-          }
-          SF_SMOOTH(0);
-          break;
+        // R = 9..24 compiled for two planes only (four would spill); calls
+        // with a YY amplitude take the run-time radius kernel
+        case 9: if (!amp_yy) { SF_SMOOTH2(9); break; } SF_SMOOTH(0); break;
+        case 10: if (!amp_yy) { SF_SMOOTH2(10); break; } SF_SMOOTH(0); break;
+        case 11: if (!amp_yy) { SF_SMOOTH2(11); break; } SF_SMOOTH(0); break;
+        case 12: if (!amp_yy) { SF_SMOOTH2(12); break; } SF_SMOOTH(0); break;
+        case 13: if (!amp_yy) { SF_SMOOTH2(13); break; } SF_SMOOTH(0); break;
+        case 14: if (!amp_yy) { SF_SMOOTH2(14); break; } SF_SMOOTH(0); break;
+        case 15: if (!amp_yy) { SF_SMOOTH2(15); break; } SF_SMOOTH(0); break;
+        case 16: if (!amp_yy) { SF_SMOOTH2(16); break; } SF_SMOOTH(0); break;
+        case 17: if (!amp_yy) { SF_SMOOTH2(17); break; } SF_SMOOTH(0); break;
+        case 18: if (!amp_yy) { SF_SMOOTH2(18); break; } SF_SMOOTH(0); break;
+        case 19: if (!amp_yy) { SF_SMOOTH2(19); break; } SF_SMOOTH(0); break;
+        case 20: if (!amp_yy) { SF_SMOOTH2(20); break; } SF_SMOOTH(0); break;
+        case 21: if (!amp_yy) { SF_SMOOTH2(21); break; } SF_SMOOTH(0); break;
+        case 22: if (!amp_yy) { SF_SMOOTH2(22); break; } SF_SMOOTH(0); break;
+        case 23: if (!amp_yy) { SF_SMOOTH2(23); break; } SF_SMOOTH(0); break;
+        case 24: if (!amp_yy) { SF_SMOOTH2(24); break; } SF_SMOOTH(0); break;
         default: SF_SMOOTH(0);
       }
 #undef SF_SMOOTH

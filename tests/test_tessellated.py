@@ -331,6 +331,7 @@ def test_tess_gather_amplitudes_nan_byteswap(n, S):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("nx,ny,sigma", [(17, 17, 0.5), (53, 37, 1.3), (128, 128, 0.0),
+                                         (96, 40, 2.5), (40, 96, 5.0),
                                          (300, 260, 4.0), (64, 64, 6.0), (20, 9, 0.3)])
 def test_tess_kernels_agree_with_tile_kernel(nx, ny, sigma):
     """The table + gather (R = 0) and wide-tile smoothing (R <= 24) kernels
