@@ -1,7 +1,7 @@
 #!/bin/bash
 # Final-binary check: the full GPU suite, smoke(), the default bench.
 set -e
-O=gpurun_out/r2zk
+O=gpurun_out/r2zp
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/gputests.log 2>&1
