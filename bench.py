@@ -105,6 +105,9 @@ def parse():
     ap.add_argument("--tess-waves", type=int, default=0,
                     help="SF_OPT_TESS_WAVES: waves per workgroup of the "
                          "unsmoothed tessellated fill (0 = library default)")
+    ap.add_argument("--tess-gain", action="store_true",
+                    help="--screen tess: XX / YY amplitudes too (four "
+                         "distinct planes, A cos / A sin)")
     ap.add_argument("--smooth-pix", type=float, default=0.0,
                     help="--screen tess: Gaussian sigma in pixels (<= 6: "
                          "fused in the fill kernel); 0 = make_aterm_image's "
@@ -421,9 +424,17 @@ def tess_steps(args, ctx, torch, dev, dist, world, rank, coll_dev, sol, setup,
         ctx.set_option(SF_OPT_TESS_WAVES, args.tess_waves)
     flags = SF_EVAL_NAN_SCRUB
 
+    amp = {}
+    if args.tess_gain:
+        # synthetic amplitudes around 1 (log10 sigma 0.1), one set per pol
+        g = torch.Generator(device="cpu").manual_seed(7)
+        for k in ("amp_xx", "amp_yy"):
+            amp[k] = (10.0 ** (0.1 * torch.randn((S, D), generator=g,
+                                                 dtype=torch.float64))).to(dev)
+
     def step():
         ctx.tess_fill(lab_d, N, N, ph, D, S, out, ring_slots=ring,
-                      smooth_pix=args.smooth_pix, flags=flags)
+                      smooth_pix=args.smooth_pix, flags=flags, **amp)
 
     for _ in range(args.warmup):
         step()
@@ -453,7 +464,7 @@ def tess_steps(args, ctx, torch, dev, dist, world, rank, coll_dev, sol, setup,
     # without smoothing (unit amplitudes), and the first slot vs a gather
     chk = out[: min(ring, 16)].double()
     unit_err = (float((chk[:, 0] ** 2 + chk[:, 1] ** 2 - 1).abs().max())
-                if args.smooth_pix == 0 else None)
+                if args.smooth_pix == 0 and not args.tess_gain else None)
     one = torch.empty((1, 4, N, N), dtype=torch.float32, device=dev)
     ctx.tess_fill(lab_d, N, N, ph[:1], D, 1, one, smooth_pix=0.0, flags=flags)
     p0 = ph[0].cpu().numpy()
@@ -468,7 +479,8 @@ def tess_steps(args, ctx, torch, dev, dist, world, rank, coll_dev, sol, setup,
                   else "kl_tess_smooth_kernel")
         # PMC traffic (profiles/traffic.json) when measured on this call shape
         traffic = None
-        wkey = args.workload + "-tess" + (f"-s{args.smooth_pix:g}" if args.smooth_pix else "")
+        wkey = (args.workload + "-tess" + ("-gain" if args.tess_gain else "")
+                + (f"-s{args.smooth_pix:g}" if args.smooth_pix else ""))
         tj = _profile_entry("traffic.json", wkey, kernel)
         if (tj is not None and tj.get("flags") == flags
                 and abs(tj.get("algorithmic_bytes_per_launch", 0) - bytes_launch)
@@ -486,7 +498,8 @@ def tess_steps(args, ctx, torch, dev, dist, world, rank, coll_dev, sol, setup,
             "config": {
                 "workload": (f"{args.workload}-tess: {A_total} ant x {T} time x {F} "
                              f"freq x {D} dir, {A} ant per GPU, tessellated "
-                             f"(Voronoi) {N}^2 screen, smooth {args.smooth_pix} px"),
+                             f"(Voronoi) {N}^2 screen, smooth {args.smooth_pix} px"
+                             + (", XX / YY amplitudes" if args.tess_gain else "")),
                 "screen": "tess", "slots_per_gpu": S, "grid": N, "n_dir": D,
                 "parallelism": f"ant-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,

@@ -581,11 +581,12 @@ int launch_tess(sf_ctx* ctx, const int32_t* labels, int nx, int ny,
         case 6: SF_SMOOTH(6); break;
         case 7: SF_SMOOTH(7); break;
         case 8: SF_SMOOTH(8); break;
-        // R = 9..24 compiled for two planes only (four would spill); calls
-        // with a YY amplitude take the run-time radius kernel
-        case 9: if (!amp_yy) { SF_SMOOTH2(9); break; } SF_SMOOTH(0); break;
-        case 10: if (!amp_yy) { SF_SMOOTH2(10); break; } SF_SMOOTH(0); break;
-        case 11: if (!amp_yy) { SF_SMOOTH2(11); break; } SF_SMOOTH(0); break;
+        // R = 9..11 compiled for both plane counts, 12..24 for two planes
+        // only (four would spill); four-plane calls there take the run-time
+        // radius kernel
+        case 9: SF_SMOOTH(9); break;
+        case 10: SF_SMOOTH(10); break;
+        case 11: SF_SMOOTH(11); break;
         case 12: if (!amp_yy) { SF_SMOOTH2(12); break; } SF_SMOOTH(0); break;
         case 13: if (!amp_yy) { SF_SMOOTH2(13); break; } SF_SMOOTH(0); break;
         case 14: if (!amp_yy) { SF_SMOOTH2(14); break; } SF_SMOOTH(0); break;
