@@ -20,6 +20,7 @@ Prints ONE JSON line on rank 0.
 import argparse
 import json
 import os
+import socket
 import sys
 import time
 
@@ -61,11 +62,13 @@ def parse():
                          "|err| <= 2.3e-7)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fits", action="store_true",
-                    help="skip the FITS-cube wall-clock leg (configs 1-2)")
+                    help="skip the FITS-cube wall-clock legs (configs 1-3)")
+    ap.add_argument("--no-fits-config3", action="store_true",
+                    help="skip only the config-3 (107 GB, KL 256^2) FITS leg")
     ap.add_argument("--cpu-workers", type=int, default=0,
-                    help="CPU baseline pool size; 0 (default): every CPU this "
-                         "process may run on, capped at the 16 host cores a "
-                         "one-GPU box grants per GPU")
+                    help="CPU baseline pool size; 0 (default): this GPU's "
+                         "share of the host (affinity / GPUs per node, capped "
+                         "by OMP_NUM_THREADS), see cpu_share()")
     ap.add_argument("--no-side-legs", action="store_true",
                     help="skip the untimed side measurements (fp64-sincos "
                          "eval, fit alone on the whole chip)")
@@ -137,8 +140,10 @@ def parse():
 # CPU baseline: the oracle (numpy fp64 restatement of the reference) on a
 # bounded slot sample, in a pool of single-threaded workers.
 # --------------------------------------------------------------------------
+_BLAS_THREADS = ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")
+
+
 def _cpu_worker(job):
-    os.environ["OMP_NUM_THREADS"] = "1"
     sys.path.insert(0, REPO)
     from oracle import kl as okl  # test infrastructure: baseline leg only
 
@@ -162,7 +167,7 @@ def _cpu_worker(job):
     return phi.shape[0], t_fit, n_eval, t_eval
 
 
-def cpu_baseline(sol, setup, n_workers, slots_fit=64, slots_eval=192):
+def cpu_baseline(sol, setup, n_workers, rule="", slots_fit=64, slots_eval=192):
     import multiprocessing as mp
 
     T, F, A, D = sol.val.shape
@@ -178,10 +183,21 @@ def cpu_baseline(sol, setup, n_workers, slots_fit=64, slots_eval=192):
                      [setup["st_order"][a]] * len(ts), setup["piercepoints"],
                      (setup["x"], setup["y"]), slots_eval))
     ctx = mp.get_context("spawn")
-    t0 = time.perf_counter()
-    with ctx.Pool(n_workers) as pool:
-        res = pool.map(_cpu_worker, jobs)
-    wall = time.perf_counter() - t0
+    # single-threaded BLAS in every worker: the spawned interpreters read the
+    # thread counts from the environment when they import numpy
+    saved = {k: os.environ.get(k) for k in _BLAS_THREADS}
+    os.environ.update({k: "1" for k in _BLAS_THREADS})
+    try:
+        t0 = time.perf_counter()
+        with ctx.Pool(n_workers) as pool:
+            res = pool.map(_cpu_worker, jobs)
+        wall = time.perf_counter() - t0
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     n_fit = sum(r[0] for r in res)
     t_fit = sum(r[1] for r in res)
     n_ev = sum(r[2] for r in res)
@@ -196,6 +212,7 @@ def cpu_baseline(sol, setup, n_workers, slots_fit=64, slots_eval=192):
         "value": n_workers / per_slot,
         "unit": "screen-slots/s",
         "cores": n_workers,
+        "cores_rule": rule,
         "kind": "port",
         "host_cpus": os.cpu_count(),
         "affinity_cpus": _affinity(),
@@ -222,11 +239,77 @@ def _affinity():
         return os.cpu_count()
 
 
-def fits_wallclock():
-    """FITS-cube wall-clock of make_aterm_image on the reference fixture:
-    config 1 (tessellated 17^2, smooth 0.1 deg) and config 2 (KL 128^2);
-    fit + evaluation + FITS write, host I/O included (second run of each,
-    i.e. with the device context warm)."""
+def _node_gpus():
+    """GPUs of the node (not just the ones this process sees): KFD topology
+    nodes with a non-zero gfx_target_version; 8 (an MI355X node) when the
+    topology is not readable."""
+    root = "/sys/class/kfd/kfd/topology/nodes"
+    n = 0
+    try:
+        for d in os.listdir(root):
+            try:
+                txt = open(os.path.join(root, d, "properties")).read()
+            except OSError:
+                continue
+            for ln in txt.splitlines():
+                k, _, v = ln.partition(" ")
+                if k == "gfx_target_version" and v.strip() not in ("", "0"):
+                    n += 1
+    except OSError:
+        pass
+    return n or 8
+
+
+def cpu_share():
+    """CPU-baseline pool size: this GPU's share of the host's cores = the
+    CPUs this process may run on / the node's GPUs, capped by
+    OMP_NUM_THREADS when the job sets it (the GPU box grants 16 host threads
+    per GPU that way).  Returns (workers, rule)."""
+    aff = _affinity() or 1
+    gpus = _node_gpus()
+    share = max(1, aff // gpus)
+    rule = f"affinity {aff} CPUs / {gpus} GPUs per node = {share}"
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and 0 < int(omp) < share:
+        share = int(omp)
+        rule += f", capped by OMP_NUM_THREADS={omp} (the job's per-GPU CPU grant)"
+    return share, rule
+
+
+def file_write_ceiling(outdir, nbytes, block=1 << 30):
+    """The box's file-write rate where the FITS legs write: ``nbytes`` of one
+    pre-filled buffer written in ``block`` pieces by plain ``write`` calls
+    (what the FITS writer does), then closed; the unlink timed apart."""
+    buf = memoryview(np.full(block, 0x3F, np.uint8))
+    path = os.path.join(outdir, "write_ceiling.bin")
+    t0 = time.perf_counter()
+    with open(path, "wb") as fh:
+        left = nbytes
+        while left > 0:
+            fh.write(buf[:min(block, left)])
+            left -= block
+    dt = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    os.remove(path)
+    return {"bytes": nbytes, "wall_s": dt, "GB_per_s": nbytes / dt / 1e9,
+            "unlink_s": time.perf_counter() - t1,
+            "what": "plain write() of one buffer in 1 GiB pieces, same directory"}
+
+
+def fits_wallclock(config3=True):
+    """FITS-cube wall-clock of make_aterm_image (the second half of the
+    BASELINE.json metric; fit + evaluation + FITS write, host I/O included):
+
+    * config 1 (tessellated 17^2, smooth 0.1 deg) and config 2 (KL 128^2) on
+      the reference fixture, best of two runs (the second with the device
+      context warm);
+    * config 3, the KL 256^2 cube of 64 ant x 100 t x 16 f x 20 dir (107.4 GB,
+      synthetic solutions): one run, written as the reference writes a cube
+      larger than memory -- one FITS file per time chunk (screen.py:283-317) --
+      10 times (10.7 GB) per file, each file deleted when closed (the box has
+      less disk than the cube); the unlink time is reported apart, and the
+      box's plain file-write rate over one chunk's bytes is measured in the
+      same directory right after."""
     import tempfile
     sys.path.insert(0, os.path.join(REPO, "tools"))
     import fits_wallclock as fw
@@ -239,7 +322,68 @@ def fits_wallclock():
             best = r if best is None or r["wall_s"] < best["wall_s"] else best
         res[name] = {"wall_s": best["wall_s"], "fits_bytes": best["fits_bytes"],
                      "screen_type": best["screen_type"],
-                     "grid": 17 if name == "config1" else 128}
+                     "grid": 17 if name == "config1" else 128,
+                     "slots": best["slots"], "slots_per_s": best["slots_per_s"],
+                     "fits_GB_per_s": best["fits_GB_per_s"]}
+    if config3:
+        with tempfile.TemporaryDirectory() as src:
+            h5, slots = fw.synthetic_npz("config3", src)
+            with tempfile.TemporaryDirectory() as d:
+                r = fw.run("config3", d, h5, slots)
+                ceil = file_write_ceiling(d, r["fits_bytes"] // r["files"])
+        res["config3"] = {
+            "screen_type": "kl", "grid": 256, "slots": slots,
+            "wall_s": r["wall_s"], "unlink_s": r["unlink_s"],
+            "wall_s_without_unlink": r["wall_s_without_unlink"],
+            "fits_bytes": r["fits_bytes"], "files": r["files"],
+            "fits_GB_per_s": r["fits_GB_per_s"],
+            "fits_GB_per_s_without_unlink": r["fits_GB_per_s_without_unlink"],
+            "slots_per_s": slots / r["wall_s"],
+            "file_write_ceiling": ceil,
+            "frac_of_file_write_ceiling":
+                r["fits_GB_per_s_without_unlink"] / ceil["GB_per_s"],
+            "what": ("make_aterm_image(screen_type='kl', cellsize_deg=0.01301) "
+                     "on synthetic 64 ant x 100 t x 16 f x 20 dir solutions: "
+                     "fit + eval + big-endian FITS, 10 time-chunk files of "
+                     "10.7 GB, each deleted after close")}
+    return res
+
+
+def cpu_reference_path(cases=("config1", "config2")):
+    """BASELINE.json configs[0] / [1] on the CPU, one core (``ncpu=1``): the
+    oracle's make_aterm_image path (oracle/pipeline.py: fit, evaluation or
+    Voronoi gather + smoothing, FITS write) on the reference fixture, each in
+    a child process pinned to one CPU with single-threaded BLAS.  Beside it
+    the reference's own timings on the same fixture measured in the survey
+    (SURVEY.md §6, 8-vCPU Xeon, ncpu=1)."""
+    import subprocess
+    import tempfile
+    cpu = sorted(os.sched_getaffinity(0))[-1] if hasattr(os, "sched_getaffinity") else 0
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1",
+               MKL_NUM_THREADS="1", SF_PIN_CPU=str(cpu))
+    # survey: VoronoiScreen.write 1.40 s (17^2, smooth 0.5 px);
+    # stationscreen.run 2.80 s + calculate_kl_screen 8.5 us / pixel / slot
+    ref_s = {"config1": 1.40, "config2": 2.80 + 8.5e-6 * 128 * 128 * 14880}
+    res = {}
+    for case in cases:
+        with tempfile.TemporaryDirectory() as d:
+            p = subprocess.run([sys.executable, "-m", "oracle.pipeline", case, d],
+                               cwd=REPO, env=env, capture_output=True, text=True,
+                               timeout=300)
+        if p.returncode != 0:
+            res[case] = {"error": p.stderr[-400:]}
+            continue
+        r = json.loads(p.stdout.strip().splitlines()[-1])
+        r["slots_per_s"] = r["slots"] / r["wall_s"]
+        r["cores"] = 1
+        r["kind"] = "port"
+        r["reference_calibration_s"] = ref_s[case]
+        r["reference_calibration_note"] = (
+            "survey measurement of the reference itself, ncpu=1 (SURVEY.md §6): "
+            + ("VoronoiScreen.write, 17^2, smooth 0.5 px" if case == "config1" else
+               "stationscreen.run 2.80 s + calculate_kl_screen at 8.5 us / pixel "
+               "/ slot x 128^2 x 14,880 slots (extrapolated from its 17^2 run)"))
+        res[case] = r
     return res
 
 
@@ -292,6 +436,19 @@ def sampled_slots_check(ctx, torch, dev, setup, coef, N, flags, slot_sums,
         res["checksums_match"] = bool(sums_ok)
         res["ok"] = res["ok"] and bool(sums_ok)
     return res
+
+
+def dist_block(args, world, record):
+    """The line's ``dist`` object: backend, world size, every rank's device
+    identity (index, PCI address, UUID, host) and its own numbers (slots,
+    mean eval-launch time, wall time of the timed steps), gathered from all
+    ranks after the timed region."""
+    from ska_sdp_screen_fitting_amd.distributed import gather_records
+    per_rank = gather_records(record)
+    devs = args.idents
+    return {"backend": args.dist_backend if world > 1 else "none",
+            "world": world, "devices": devs, "per_rank": per_rank,
+            "distinct_devices": len({d.get("uuid") or d.get("pci") for d in devs})}
 
 
 FP64_MFMA_PEAK_TFS = 78.6  # MI355X fp64 matrix peak (AMD spec, dense)
@@ -455,16 +612,27 @@ def tess_steps(args, ctx, torch, dev, dist, world, rank, coll_dev, sol, setup,
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    local_elapsed = elapsed
     tmax = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
     if world > 1:
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     elapsed = tmax.item()
     launch_s = float(np.mean([a.elapsed_time(b) for a, b in evs])) * 1e-3
-    # parity spot check of the last ring slots (not timed): cos^2 + sin^2 = 1
-    # without smoothing (unit amplitudes), and the first slot vs a gather
+    dist_info = dist_block(args, world, {
+        "rank": rank, "slots": S, "fill_launch_ms": launch_s * 1e3,
+        "steps_wall_s": local_elapsed, "device_pci": args.idents[rank]["pci"]})
+    # parity spot check of the last ring slots (not timed), without
+    # smoothing: cos^2 + sin^2 = 1 (unit amplitudes), or with XX / YY
+    # amplitudes the shared angle (Re XX Im YY - Im XX Re YY = 0 relative to
+    # |XX| |YY|); and the first slot vs a gather
     chk = out[: min(ring, 16)].double()
-    unit_err = (float((chk[:, 0] ** 2 + chk[:, 1] ** 2 - 1).abs().max())
-                if args.smooth_pix == 0 and not args.tess_gain else None)
+    unit_err, check_name = None, "max_abs_cos2_plus_sin2_minus_1"
+    if args.smooth_pix == 0 and not args.tess_gain:
+        unit_err = float((chk[:, 0] ** 2 + chk[:, 1] ** 2 - 1).abs().max())
+    elif args.smooth_pix == 0:
+        cross = chk[:, 0] * chk[:, 3] - chk[:, 1] * chk[:, 2]
+        mag = (chk[:, 0].hypot(chk[:, 1]) * chk[:, 2].hypot(chk[:, 3])).clamp(min=1e-30)
+        unit_err, check_name = float((cross / mag).abs().max()), "max_rel_xx_yy_angle_cross"
     one = torch.empty((1, 4, N, N), dtype=torch.float32, device=dev)
     ctx.tess_fill(lab_d, N, N, ph[:1], D, 1, one, smooth_pix=0.0, flags=flags)
     p0 = ph[0].cpu().numpy()
@@ -507,8 +675,9 @@ def tess_steps(args, ctx, torch, dev, dist, world, rank, coll_dev, sol, setup,
                          "traffic": traffic, "kernel": kernel,
                          "bytes_per_launch": bytes_launch,
                          "launch_ms": launch_s * 1e3},
-            "check": {"max_abs_cos2_plus_sin2_minus_1": unit_err,
+            "check": {check_name: unit_err,
                       "slot0_max_ulp_vs_numpy_gather": ulp},
+            "dist": dist_info,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -535,6 +704,19 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
+    # which physical GPU every rank drives, gathered once before any work:
+    # under nccl two ranks on one card end the job here
+    from ska_sdp_screen_fitting_amd.distributed import (check_distinct_devices,
+                                                        device_identity,
+                                                        gather_records)
+    ident = dict(device_identity(torch, dev), rank=rank, local_rank=local_rank,
+                 host=socket.gethostname())
+    idents = gather_records(ident)
+    try:
+        check_distinct_devices(idents, args.dist_backend if world > 1 else "none")
+    except RuntimeError as exc:
+        raise SystemExit(f"bench.py: {exc}")
+    args.idents = idents
 
     from ska_sdp_screen_fitting_amd import get_context
     from ska_sdp_screen_fitting_amd._lib import (SF_EVAL_FAST_SINCOS,
@@ -749,6 +931,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    local_elapsed = elapsed
     ctx.set_stream(stream.cuda_stream)
     fit_stats = ctx.fit_stats() if not args.eval_only else {}
     # per-step stage sums; per-launch eval duration for the roofline
@@ -761,9 +944,23 @@ def main():
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     elapsed = tmax.item()
 
-    # parity spot check (cheap invariants, not timed): cos^2 + sin^2 = 1
-    chk = out[: min(ring, 64)].float()
-    unit_err = float((chk[:, 0] ** 2 + chk[:, 1] ** 2 - 1).abs().max())
+    dist_info = dist_block(args, world, {
+        "rank": rank, "slots": S, "eval_launch_ms": t_eval_launch * 1e3,
+        "fit_ms_per_step": t_fit * 1e3, "steps_wall_s": local_elapsed,
+        "device_pci": args.idents[rank]["pci"]})
+    # parity spot check (cheap invariants, not timed): per screen type, the
+    # invariant of its planes -- phase screens cos^2 + sin^2 = 1; gain screens
+    # Re XX / Im XX and Re YY / Im YY share an angle, so
+    # Re XX * Im YY - Im XX * Re YY = 0 relative to |XX| |YY|
+    chk = out[: min(ring, 64)].double()
+    if gain:
+        cross = chk[:, 0] * chk[:, 3] - chk[:, 1] * chk[:, 2]
+        mag = (chk[:, 0].hypot(chk[:, 1]) * chk[:, 2].hypot(chk[:, 3])).clamp(min=1e-30)
+        check_name = "max_rel_xx_yy_angle_cross"
+        unit_err = float((cross / mag).abs().max())
+    else:
+        check_name = "max_abs_cos2_plus_sin2_minus_1"
+        unit_err = float((chk[:, 0] ** 2 + chk[:, 1] ** 2 - 1).abs().max())
     sampled = sampled_slots_check(
         ctx, torch, dev, setup, coef.reshape(-1, D), N, flags, slot_sums,
         args.warmup + args.steps, not args.precise_sincos,
@@ -839,8 +1036,8 @@ def main():
                           "overlap": "fit(c+1) || eval(c), %d time chunks" % n_chunks
                           if n_chunks > 1 else "none"},
             "fit_stats": fit_stats,
-            "check": {"max_abs_cos2_plus_sin2_minus_1": unit_err,
-                      "sampled_slots": sampled},
+            "check": {check_name: unit_err, "sampled_slots": sampled},
+            "dist": dist_info,
         }
         if side:
             line["side_legs"] = side
@@ -867,10 +1064,21 @@ def main():
                                 for k, v in (fe or {}).get("kernels", {}).items()},
             }
         if not args.no_fits and world == 1:
-            line["fits_wallclock"] = fits_wallclock()
+            line["fits_wallclock"] = fits_wallclock(config3=not args.no_fits_config3)
         if not args.no_cpu_baseline and world == 1:
-            nw = args.cpu_workers or min(16, _affinity() or 1)
-            line["cpu_baseline"] = cpu_baseline(sol, setup, max(1, nw))
+            nw, rule = cpu_share()
+            if args.cpu_workers:
+                nw, rule = args.cpu_workers, "--cpu-workers"
+            line["cpu_baseline"] = cpu_baseline(sol, setup, max(1, nw), rule)
+            # BASELINE.json configs[0] / [1]: the CPU path of make_aterm_image
+            # on one core, next to fits_wallclock.config1 / config2
+            legs = cpu_reference_path()
+            fw = line.get("fits_wallclock", {})
+            for k, v in legs.items():
+                if k in fw and "wall_s" in v:
+                    v["gpu_fits_wall_s"] = fw[k]["wall_s"]
+                    v["gpu_speedup"] = v["wall_s"] / fw[k]["wall_s"]
+            line["cpu_baseline"]["legs"] = legs
         print(json.dumps(line), flush=True)
     # release the CU-masked stream before the HIP runtime tears down
     torch.cuda.synchronize(dev)

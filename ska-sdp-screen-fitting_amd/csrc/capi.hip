@@ -457,12 +457,16 @@ int sf_kl_eval_sums(sf_ctx* ctx, const double* coef_phase,
 }
 
 // scipy.ndimage._gaussian_kernel1d(sigma, 0, int(4 sigma + 0.5)) uploaded to
-// ctx->d_gw (stream-ordered); R = 0 for sigma <= 1e-15
+// ctx->d_gw; R = 0 for sigma <= 1e-15 (the one weight 1.0).  The weights of
+// the last sigma stay on the device: repeated calls with the same sigma (every
+// chunk of a Screen.write) upload nothing and stay fully asynchronous.
 static int upload_gaussian(sf_ctx* ctx, double sigma, int* R_out) {
-  int R = 0;
+  if (sigma <= 1e-15) sigma = 0.0;
+  const int R = sigma > 0.0 ? (int)(4.0 * sigma + 0.5) : 0;
+  *R_out = R;
+  if (ctx->d_gw && sigma == ctx->gw_sigma) return SF_OK;
   std::vector<double> w(1, 1.0);
-  if (sigma > 1e-15) {
-    R = (int)(4.0 * sigma + 0.5);
+  if (sigma > 0.0) {
     w.assign(2 * R + 1, 0.0);
     double sum = 0.0;
     for (int i = -R; i <= R; ++i)
@@ -470,6 +474,10 @@ static int upload_gaussian(sf_ctx* ctx, double sigma, int* R_out) {
     for (int i = 0; i < 2 * R + 1; ++i) sum += w[i];
     for (int i = 0; i < 2 * R + 1; ++i) w[i] /= sum;
   }
+  // new weights (a change of sigma, rare): launches on ANY stream may still
+  // read the previous ones, and the host vector dies here -- drain the
+  // device, copy on the context's stream, wait for the copy
+  SF_HIP(hipDeviceSynchronize());
   if (ctx->gw_cap < w.size()) {
     if (ctx->d_gw) (void)hipFree(ctx->d_gw);
     ctx->d_gw = nullptr;
@@ -482,12 +490,10 @@ static int upload_gaussian(sf_ctx* ctx, double sigma, int* R_out) {
     }
     ctx->gw_cap = cap;
   }
-  // a synchronous copy: the host vector dies here and an earlier launch on
-  // the stream may still read the previous weights
+  SF_HIP(hipMemcpyAsync(ctx->d_gw, w.data(), w.size() * sizeof(double),
+                        hipMemcpyHostToDevice, ctx->stream));
   SF_HIP(hipStreamSynchronize(ctx->stream));
-  SF_HIP(hipMemcpy(ctx->d_gw, w.data(), w.size() * sizeof(double),
-                   hipMemcpyHostToDevice));
-  *R_out = R;
+  ctx->gw_sigma = sigma;
   return SF_OK;
 }
 

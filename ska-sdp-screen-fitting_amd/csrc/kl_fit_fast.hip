@@ -1022,7 +1022,14 @@ int launch_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,
   SF_HIP(hipMemcpyAsync(&err, ctx->d_counters + 3, sizeof(int),
                         hipMemcpyDeviceToHost, ctx->stream));
   SF_HIP(hipStreamSynchronize(ctx->stream));
-  SF_REQUIRE(err == 0, SF_EIO, "sf_kl_fit: internal mask table overflow");
+  // error bits of the fit pass: 1 / 2 the mask table (lookup miss / subset
+  // basis missing), 4 the lean layout met a slot whose unflagged weights are
+  // not uniform (kl_classify_kernel counted it uniform: an internal
+  // inconsistency, the slot was left unwritten)
+  SF_REQUIRE((err & 3) == 0, SF_EIO, "sf_kl_fit: internal mask table overflow");
+  SF_REQUIRE((err & 4) == 0, SF_EIO,
+             "sf_kl_fit: lean fit pass saw non-uniform weights in a slot "
+             "classified uniform (slot left unwritten)");
   return SF_OK;
 }
 

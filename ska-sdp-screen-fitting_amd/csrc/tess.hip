@@ -26,12 +26,12 @@ constexpr int kMaxR = kTessMaxR;  // fused-tile Gaussian radius (sigma <= 6 px)
 constexpr int kTessSlots = 64;  // slots per workgroup
 
 __device__ __forceinline__ int reflect_idx(int i, int n) {
-  // scipy.ndimage mode 'reflect': d c b a | a b c d | d c b a
-  while (i < 0 || i >= n) {
-    if (i < 0) i = -i - 1;
-    if (i >= n) i = 2 * n - i - 1;
-  }
-  return i;
+  // scipy.ndimage mode 'reflect' (d c b a | a b c d | d c b a) in closed
+  // form: period 2n, the second half mirrored -- O(1) for any offset
+  if (i >= 0 && i < n) return i;
+  int m = i % (2 * n);
+  if (m < 0) m += 2 * n;
+  return m < n ? m : 2 * n - 1 - m;
 }
 
 __global__ __launch_bounds__(256) void kl_tess_kernel(

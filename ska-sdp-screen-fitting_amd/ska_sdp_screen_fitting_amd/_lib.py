@@ -329,9 +329,15 @@ class Context:
         ring = max(int(S if ring_slots is None else ring_slots), 1)
         n = int(S) * int(D)
         if hasattr(labels, "min") and labels.numel():
-            lo, hi = int(labels.min()), int(labels.max())
-            if lo < 1 or hi > int(D):
-                raise ValueError(f"labels: values {lo}..{hi} outside 1..{D}")
+            # validated once per label tensor (its storage, size, in-place
+            # version and D): every chunk of a Screen.write passes the same
+            # template, and min / max are two reductions + two host syncs
+            key = (labels.data_ptr(), labels.numel(), labels._version, int(D))
+            if key != getattr(self, "_labels_ok", None):
+                lo, hi = int(labels.min()), int(labels.max())
+                if lo < 1 or hi > int(D):
+                    raise ValueError(f"labels: values {lo}..{hi} outside 1..{D}")
+                self._labels_ok = key
         _check(self.lib.sf_tess_fill(
             self.h, self._dev(labels, np.int32, int(nx) * int(ny), "labels"),
             int(nx), int(ny), self._dev(phase, np.float64, n, "phase"),

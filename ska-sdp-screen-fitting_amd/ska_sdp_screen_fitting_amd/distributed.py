@@ -16,6 +16,8 @@ one-shot setup collectives over RCCL (backend "nccl") or gloo (CPU tests):
   ``ref_ant``.
 """
 
+import os
+
 import numpy as np
 
 from . import geometry
@@ -99,3 +101,41 @@ def setup_shard(local, ant_offset, n_ant_total, rad, dec, width_deg,
     return dict(ref_ant=ref, st_order=st_order, piercepoints=pp,
                 mid_ra=float(hdr[4]), mid_dec=float(hdr[5]), x=x, y=y,
                 ref_phase=refph, ant_offset=ant_offset)
+
+
+def device_identity(torch, device):
+    """Which physical GPU a rank runs on: its torch index, PCI address and
+    UUID (what ``rocm-smi`` / the kernel name the card by)."""
+    p = torch.cuda.get_device_properties(device)
+    return {"index": int(device.index if device.index is not None else 0),
+            "pci": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}",
+            "uuid": str(getattr(p, "uuid", "")), "name": p.name,
+            "visible": os.environ.get("HIP_VISIBLE_DEVICES",
+                                      os.environ.get("CUDA_VISIBLE_DEVICES"))}
+
+
+def gather_records(record, group=None):
+    """Every rank's ``record`` (a JSON-able dict), in rank order, on every
+    rank (all_gather_object; one call, outside any timed region)."""
+    import torch.distributed as dist
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return [record]
+    out = [None] * dist.get_world_size(group)
+    dist.all_gather_object(out, record, group=group)
+    return out
+
+
+def check_distinct_devices(idents, backend):
+    """Refuse a one-process-per-GPU job whose ranks share a card: under
+    nccl (RCCL) every rank must resolve to its own PCI device.  gloo
+    rehearsals may share one (their rates then mean nothing).  Raises
+    RuntimeError naming the ranks that collide."""
+    if backend != "nccl":
+        return
+    seen = {}
+    for r, d in enumerate(idents):
+        key = d.get("uuid") or d.get("pci")
+        if key in seen:
+            raise RuntimeError(f"ranks {seen[key]} and {r} resolve to the same GPU "
+                               f"({d.get('pci')}, uuid {d.get('uuid')})")
+        seen[key] = r

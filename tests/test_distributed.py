@@ -1,6 +1,7 @@
 """Antenna sharding over ranks (world_size 2, gloo on CPU): the one-shot
 setup collectives give every shard exactly what the unsharded run uses."""
 
+import json
 import os
 import socket
 
@@ -10,7 +11,9 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from ska_sdp_screen_fitting_amd.distributed import setup_shard, shard_range
+from ska_sdp_screen_fitting_amd.distributed import (check_distinct_devices,
+                                                    gather_records, setup_shard,
+                                                    shard_range)
 from ska_sdp_screen_fitting_amd.geometry import piercepoints, grid_coords
 from ska_sdp_screen_fitting_amd.stationscreen import station_orders
 from ska_sdp_screen_fitting_amd.synthetic import (FIELD_DEC_DEG, FIELD_RA_DEG,
@@ -89,6 +92,11 @@ def test_shards_are_slices_of_the_full_set():
 
 @pytest.mark.timeout(300)
 def test_setup_shard_world2_matches_unsharded(tmp_path):
+    """Every rank's setup equals the unsharded run's, and the ORACLE's fit +
+    evaluation of sampled slots from each shard's setup give the same cube
+    checksums as the same slots of the unsharded setup (the GPU side of
+    sharding: tests/test_slot_sums.py::test_sharded_gpu_sums_equal_unsharded
+    and test_gpu_parity.py::test_fit_sharded_equals_unsharded)."""
     world = 2
     mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)),
                        nprocs=world, join=True, start_method="spawn")
@@ -116,3 +124,43 @@ def test_setup_shard_world2_matches_unsharded(tmp_path):
         want = _slot_checksums(phi, full.weight, want_orders, pp, x, y, glob, ref)
         assert [int(v) for v in z["sums"]] == want
     assert got_orders == want_orders
+
+
+def _gather_worker(rank, world, port, outdir, same_card):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    bus = 0x11 if same_card else 0x11 + rank
+    ident = {"index": 0, "pci": f"0000:{bus:02x}:00", "uuid": f"GPU-{bus}",
+             "rank": rank}
+    idents = gather_records(ident)
+    rec = gather_records({"rank": rank, "slots": 100 + rank, "eval_launch_ms": 1.5 * rank})
+    try:
+        check_distinct_devices(idents, "nccl")
+        verdict = "ok"
+    except RuntimeError as exc:
+        verdict = str(exc)
+    check_distinct_devices(idents, "gloo")  # rehearsals may share a card
+    with open(os.path.join(outdir, f"g{rank}.json"), "w") as fh:
+        json.dump([idents, rec, verdict], fh)
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("same_card", [False, True])
+def test_rank_records_world2(tmp_path, same_card):
+    """bench.py's ``dist`` object: every rank's device identity and numbers
+    reach every rank in rank order; under nccl two ranks on one card are
+    refused, under gloo allowed."""
+    world = 2
+    mp.start_processes(_gather_worker,
+                       args=(world, _free_port(), str(tmp_path), same_card),
+                       nprocs=world, join=True, start_method="spawn")
+    for r in range(world):
+        idents, rec, verdict = json.load(open(tmp_path / f"g{r}.json"))
+        assert [d["rank"] for d in idents] == [0, 1]
+        assert [d["slots"] for d in rec] == [100, 101]
+        if same_card:
+            assert "ranks 0 and 1 resolve to the same GPU" in verdict
+        else:
+            assert verdict == "ok"

@@ -142,3 +142,44 @@ def test_config5_shape_streamed_slots_vs_oracle(ctx, dev):
         assert host_sums(o)[0] == got[k], k
         want = okl.eval_planes(okl.eval_phase_screens(coef_np[k:k + 1], cpix))
         np.testing.assert_allclose(o.reshape(want.shape), want, rtol=0, atol=2e-6)
+
+
+def test_sharded_gpu_sums_equal_unsharded(ctx, dev):
+    """The GPU side of antenna sharding: fit + checksum
+    evaluation of each contiguous station shard -- reference phases passed
+    in, as distributed.setup_shard hands them to a rank that does not hold
+    the reference station -- gives, slot for slot, the same cube checksums
+    as the unsharded run on one context."""
+    from ska_sdp_screen_fitting_amd import geometry
+    from ska_sdp_screen_fitting_amd.stationscreen import station_orders
+    from ska_sdp_screen_fitting_amd.synthetic import make_solutions
+    A, T, F, D, N = 12, 3, 2, 20, 64
+    s = make_solutions(n_ant=A, n_time=T, n_freq=F, n_dir=D, seed=11,
+                       flag_frac=0.05, outlier_frac=0.02)
+    pp, mra, mdec = geometry.piercepoints(s.dir_radec)
+    cell = FIELD["width"] / (N - 0.5)
+    x, y = geometry.grid_coords(FIELD["rad"], FIELD["dec"], FIELD["width"],
+                                cell, mra, mdec)
+    ref = okl.reference_station(s.weight)
+    st = station_orders(s.ant_pos, ref, min(20, D - 1))
+    ctx.set_basis(pp)
+    ctx.set_grid(x, y)
+    refph = torch.from_numpy(np.ascontiguousarray(s.val[:, :, ref, :])).to(dev)
+
+    def run(a0, a1, ref_phase):
+        ph = torch.from_numpy(np.ascontiguousarray(s.val[:, :, a0:a1])).to(dev)
+        wt = torch.from_numpy(np.ascontiguousarray(s.weight[:, :, a0:a1])).to(dev)
+        coef = torch.empty_like(ph)
+        ctx.fit(ph, wt, T, F, a1 - a0, st[a0:a1], ref_ant=ref, coef=coef,
+                ant_offset=a0, ref_phase=ref_phase)
+        n = T * F * (a1 - a0)
+        out = torch.empty((16, 4, N, N), dtype=torch.float32, device=dev)
+        sums = torch.zeros(n, dtype=torch.int32, device=dev)
+        ctx.eval_sums(coef.reshape(n, D), n, out, sums, 16, flags=1)
+        torch.cuda.synchronize()
+        return sums.cpu().numpy().view(np.uint32).reshape(T, F, a1 - a0)
+
+    full = run(0, A, None)
+    assert len(np.unique(full)) > T * F * A // 2  # distinct cubes
+    for a0, a1 in ((0, 5), (5, 12)):
+        np.testing.assert_array_equal(run(a0, a1, refph), full[:, :, a0:a1])
