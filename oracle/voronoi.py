@@ -17,15 +17,21 @@ reference:
 
 Third-party pieces: Pillow is the reference's own dependency (pinned 9.0.1;
 Pillow 8.4.0 and 12.2.0 gave identical masks on the fixture, SURVEY §8(a)
-a14).  shapely (pinned 1.8.0) is absent from every interpreter here, so its
-two uses are restated: ``polygonize`` of the finite Voronoi ridges == the
-bounded Voronoi regions of the direction points (the outer ring bounds them),
-and ``disjoint(point)`` == "strictly outside the closed convex cell" (exact
-orientation tests on float coordinates).  PARITY STATUS: the reference's
-tessellated path cannot run in this image (needs shapely), so label rasters
-are pinned only by the reference test criterion (patch pixels,
-tests/test_fit_screens.py:43-128) and the survey's probe counts; interior
-labels are otherwise unpinned.
+a14).  shapely (pinned 1.8.0, GEOS) is absent from every interpreter here, so
+its two uses are restated from their published algorithms:
+``geos_polygonize`` walks the GEOS Polygonizer's planar graph (directed-edge
+insertion order, counter-clockwise edge stars, clockwise shells; the ring
+start vertex and direction, which Pillow's outline depends on, and the
+polygon order come from it), and ``disjoint(point)`` == "strictly outside
+the closed convex cell" (exact orientation tests on float coordinates).
+scipy 1.7.1 (the reference's era) and 1.15.3 give bit-identical Voronoi
+vertices and ridge order on the fixture at every config cell size.  PARITY
+STATUS: the reference's tessellated path cannot run in this image (needs
+shapely), so label rasters are pinned by the reference test criterion
+(patch pixels, tests/test_fit_screens.py:43-128); the ring convention is a
+restatement not checked against GEOS itself, and the pixels it decides
+(2 / 289 at 0.2 deg ... 22 / 16384 at 0.02602 deg,
+profiles/round3_tess_ring_conventions.txt) stay "parity unpinned".
 """
 
 import numpy as np
@@ -93,18 +99,107 @@ def rasterize(verts, shape):
     return data
 
 
-def _cell(vor, k):
-    reg = vor.regions[vor.point_region[k]]
-    assert -1 not in reg and len(reg) >= 3
-    v = vor.vertices[reg]
-    c = v.mean(axis=0)
-    order = np.argsort(np.arctan2(v[:, 1] - c[1], v[:, 0] - c[0]))
-    ring = [tuple(map(float, p)) for p in v[order]]
-    return ring + [ring[0]]
+def _quadrant(dx, dy):
+    """geos::geom::Quadrant::quadrant: NE 0, NW 1, SW 2, SE 3."""
+    if dx >= 0:
+        return 0 if dy >= 0 else 3
+    return 1 if dy >= 0 else 2
+
+
+def _orientation(p1, p2, q):
+    """geos::algorithm::Orientation::index: +1 q left of p1->p2 (CCW), -1
+    right, 0 collinear (exact: Fraction arithmetic on the float inputs)."""
+    from fractions import Fraction as Fr
+    det = ((Fr(p2[0]) - Fr(p1[0])) * (Fr(q[1]) - Fr(p1[1]))
+           - (Fr(p2[1]) - Fr(p1[1])) * (Fr(q[0]) - Fr(p1[0])))
+    return (det > 0) - (det < 0)
+
+
+def geos_polygonize(segments):
+    """shapely.ops.polygonize of two-point LineStrings, restated from the
+    GEOS Polygonizer algorithm (operation/polygonize: PolygonizeGraph,
+    EdgeRing; the JTS design it ports):
+
+    * every line adds its directed edges in input order: de0 start -> end,
+      then de1 end -> start (PlanarGraph::add); nodes are keyed by exact
+      coordinates;
+    * around each node the outgoing edges are sorted counter-clockwise by
+      quadrant, then orientation (DirectedEdge::compareDirection), and the
+      edge arriving along outgoing edge e_k continues on e_(k+1)
+      (computeNextCWEdges): every ring keeps its face on the right;
+    * rings are collected by walking the directed edges in insertion order,
+      starting a ring at each edge not yet in one (getEdgeRings), its
+      coordinates from that edge's start node on (EdgeRing::getCoordinates);
+    * rings that are not counter-clockwise are shells (EdgeRing::isHole):
+      the polygons, in that order, exteriors exactly as walked.
+
+    No dangles or cut edges arise from the bounded ridges of a Voronoi
+    diagram closed by an outer ring of points (every ridge separates two
+    cells, or a cell and the outer face); they are asserted absent.
+    Returns a list of closed rings [(x, y), ..., first]."""
+    nodes = {}
+    des = []  # (from node key, to node key, line index)
+    for j, (a, b) in enumerate(segments):
+        a, b = (float(a[0]), float(a[1])), (float(b[0]), float(b[1]))
+        if a == b:
+            continue
+        for u, v in ((a, b), (b, a)):
+            nodes.setdefault(u, []).append(len(des))
+            des.append((u, v, j))
+    sym = [i ^ 1 for i in range(len(des))]
+    nxt = [None] * len(des)
+    import functools
+
+    def cmp(i, k):
+        (p0, p1, _), (q0, q1, _) = des[i], des[k]
+        qa = _quadrant(p1[0] - p0[0], p1[1] - p0[1])
+        qb = _quadrant(q1[0] - q0[0], q1[1] - q0[1])
+        if qa != qb:
+            return 1 if qa > qb else -1
+        return _orientation(q0, q1, p1)  # > 0: des[i] is CCW of des[k]
+
+    for key, out in nodes.items():
+        assert len(out) >= 2, "dangle"
+        out = sorted(out, key=functools.cmp_to_key(cmp))
+        for k in range(len(out)):
+            nxt[sym[out[k]]] = out[(k + 1) % len(out)]
+    ring_of = [-1] * len(des)
+    rings = []
+    for start in range(len(des)):
+        if ring_of[start] >= 0:
+            continue
+        ring, de = [], start
+        while True:
+            ring_of[de] = len(rings)
+            ring.append(des[de][0])
+            de = nxt[de]
+            if de == start:
+                break
+        rings.append(ring + [ring[0]])
+    for i in range(len(des)):
+        assert ring_of[i] != ring_of[sym[i]], "cut edge"
+    shells = []
+    for r in rings:
+        area = sum(x0 * y1 - x1 * y0 for (x0, y0), (x1, y1) in zip(r[:-1], r[1:]))
+        if area < 0:  # not CCW
+            shells.append(r)
+    return shells
+
+
+def _contains(ring, x, y):
+    """Point strictly inside a convex closed ring (either orientation)."""
+    s = [(bx - ax) * (y - ay) - (by - ay) * (x - ax)
+         for (ax, ay), (bx, by) in zip(ring[:-1], ring[1:])]
+    return all(v > 0 for v in s) or all(v < 0 for v in s)
 
 
 def label_raster(ra_deg, dec_deg, rad, dec, width, cellsize):
-    """Label template (values 1..D), shape (ny, nx)."""
+    """Label template (values 1..D), shape (ny, nx), with the cells as the
+    reference gets them from
+    shapely.ops.polygonize of the bounded Voronoi ridges
+    (voronoi_screen.py:311-349): ``geos_polygonize`` rings (orientation,
+    start vertex) rasterized in polygonize order, each labelled with the
+    direction it contains."""
     n = int(np.ceil(width / cellsize))
     crval, crpix, cdelt = (rad, dec), (n / 2.0, n / 2.0), (-cellsize, cellsize)
     ra_deg = np.asarray(ra_deg, np.float64)
@@ -116,20 +211,23 @@ def label_raster(ra_deg, dec_deg, rad, dec, width, cellsize):
                          crval, crpix, cdelt)
     fmax = sin_world2pix(min(b[2], ra_deg.min() - 0.1), max(b[3], dec_deg.max() + 0.1),
                          crval, crpix, cdelt)
-    fmin = (float(fmin[0]), float(fmin[1]))
-    fmax = (float(fmax[0]), float(fmax[1]))
     if len(xy) == 1:
-        polys = [[fmin, (fmin[0], fmax[1]), fmax, (fmax[0], fmin[1]), fmin]]
-    else:
-        nouter = 64
-        ang = np.array([np.pi / (nouter / 2.0) * i for i in range(nouter)])
-        radius = 2.0 * np.sqrt((fmax[0] - fmin[0]) ** 2 + (fmax[1] - fmin[1]) ** 2)
-        outer = xy.mean(axis=0) + radius * np.stack([np.cos(ang), np.sin(ang)], 1)
-        vor = Voronoi(np.vstack([xy, outer]))
-        polys = [_cell(vor, k) for k in range(len(xy))]
+        x0, y0 = float(fmin[0]), float(fmin[1])
+        x1, y1 = float(fmax[0]), float(fmax[1])
+        tmpl = rasterize([(x0, y0), (x0, y1), (x1, y1), (x1, y0), (x0, y0)], (n, n))
+        return tmpl.astype(np.int32), xy
+    nouter = 64
+    ang = np.array([np.pi / (nouter / 2.0) * i for i in range(nouter)])
+    radius = 2.0 * np.sqrt((float(fmax[0]) - float(fmin[0])) ** 2
+                           + (float(fmax[1]) - float(fmin[1])) ** 2)
+    outer = xy.mean(axis=0) + radius * np.stack([np.cos(ang), np.sin(ang)], 1)
+    vor = Voronoi(np.vstack([xy, outer]))
+    segs = [vor.vertices[r] for r in vor.ridge_vertices if -1 not in r]
     tmpl = np.zeros((n, n))
-    for k, verts in enumerate(polys):
-        r = rasterize(verts, (n, n)) * (k + 1)
+    for ring in geos_polygonize(segs):
+        idx = [k for k in range(len(xy)) if _contains(ring, xy[k, 0], xy[k, 1])]
+        assert len(idx) == 1
+        r = rasterize(ring, (n, n)) * (idx[0] + 1)
         filled = r > 0
         tmpl[filled] = r[filled]
     zero = np.where(tmpl == 0)

@@ -79,16 +79,28 @@ def rasterize_cell(ring, n):
 
 def tessellation_template(patch_radec, rad, dec, width_deg, cellsize_deg):
     """voronoi_screen.py:218-351 -> (labels [ny, nx] int32 in 1..D, patch xy).
-    Cells are painted in direction order (later cells win a shared pixel)."""
-    rings, xy, n = _rings(patch_radec, rad, dec, width_deg, cellsize_deg)
-    return paint_cells(rings, n), xy
+    Cells are painted in shapely.ops.polygonize order (later cells win a
+    shared pixel)."""
+    rings, xy, n, order = _rings(patch_radec, rad, dec, width_deg, cellsize_deg)
+    return paint_cells(rings, n, order), xy
 
 
 def _rings(patch_radec, rad, dec, width_deg, cellsize_deg):
     """Voronoi cell rings in pixel coordinates (voronoi_screen.py:230-309):
     SIN pixel positions of the patches, the field box, a 64-point outer ring
-    closing the tessellation; each direction's bounded region, its vertices
-    in counter-clockwise angle order about their mean."""
+    closing the tessellation; each direction's bounded region as
+    ``shapely.ops.polygonize`` of the bounded ridges returns it (:311-317).
+
+    The ring convention follows the GEOS Polygonizer algorithm (restated
+    literally, as a graph walk, in oracle/voronoi.py::geos_polygonize): every
+    ridge j = (a, b) of ``ridge_vertices`` adds directed edges 2j (a -> b)
+    and 2j + 1 (b -> a); a ring keeps its face on the right, so a cell's
+    exterior is clockwise; it starts at the start vertex of the lowest-index
+    directed edge that bounds the cell, and the polygons come out in the
+    order of those indices.  Pillow's outline (and so the outline pixels
+    the exact test sees) depends on the ring's start and direction, and the
+    painting order on the polygon order.  Returns (rings in direction order,
+    xy, n, painting order of the directions)."""
     n = geometry.grid_size(width_deg, cellsize_deg)
     crval, crpix, cdelt = (rad, dec), (n / 2.0, n / 2.0), (-cellsize_deg, cellsize_deg)
     ra = np.asarray(patch_radec, np.float64)[:, 0]
@@ -109,31 +121,51 @@ def _rings(patch_radec, rad, dec, width_deg, cellsize_deg):
         ring_pts = xy.mean(axis=0) + radius * np.stack(
             [np.cos(np.pi / 32.0 * k), np.sin(np.pi / 32.0 * k)], axis=1)
         vor = Voronoi(np.vstack([xy, ring_pts]))
+        # lowest directed-edge index (and its start vertex) bounding each cell
+        first = {}
+        j = 0
+        for (va, vb), (p, q) in zip(vor.ridge_vertices, vor.ridge_points):
+            if va == -1 or vb == -1:
+                continue
+            a, b = vor.vertices[va], vor.vertices[vb]
+            for c in (p, q):
+                if c < len(xy):
+                    # cell c on the right of a -> b: the forward edge 2j
+                    right = ((b[0] - a[0]) * (xy[c, 1] - a[1])
+                             - (b[1] - a[1]) * (xy[c, 0] - a[0])) < 0
+                    de, start = (2 * j, va) if right else (2 * j + 1, vb)
+                    if c not in first or de < first[c][0]:
+                        first[c] = (de, start)
+            j += 1
         rings = []
         for i in range(len(xy)):
             reg = vor.regions[vor.point_region[i]]
-            if -1 in reg:
+            if -1 in reg or i not in first:
                 raise ValueError("unbounded Voronoi cell for a direction")
             v = vor.vertices[reg]
             ctr = v.mean(axis=0)
-            v = v[np.argsort(np.arctan2(v[:, 1] - ctr[1], v[:, 0] - ctr[0]))]
-            pts = [(float(a), float(b)) for a, b in v]
+            cw = np.argsort(-np.arctan2(v[:, 1] - ctr[1], v[:, 0] - ctr[0]))
+            idx = [reg[k] for k in cw]
+            k0 = idx.index(first[i][1])
+            idx = idx[k0:] + idx[:k0]
+            pts = [(float(vor.vertices[k][0]), float(vor.vertices[k][1])) for k in idx]
             rings.append(pts + [pts[0]])
-    return rings, xy, n
+        order = sorted(range(len(xy)), key=lambda c: first[c][0])
+        return rings, xy, n, order
+    return rings, xy, n, [0]
 
 
-def paint_cells(rings, n):
+def paint_cells(rings, n, order=None):
     """voronoi_screen.py:319-349: rasterize every cell ring (label = index +
-    1) in list order -- a pixel claimed by two cells (its centre exactly on
-    their shared edge: the exact border test keeps it in both) takes the
-    later one -- then give uncovered pixels the nearest painted label
-    (griddata 'nearest' in index space).  The reference paints in shapely
-    polygonize order (GEOS's edge-ring order, not reproducible here); on the
-    fixture no pixel is claimed twice at 0.2, 0.1, 0.05 or 0.02602 deg
-    (tests/test_tessellated.py), so the order does not matter there."""
+    1) in ``order`` (default: list order; the reference paints in polygonize
+    order) -- a pixel claimed by two cells (its centre exactly on their
+    shared edge: the exact border test keeps it in both) takes the later one
+    -- then give uncovered pixels the nearest painted label (griddata
+    'nearest' in index space).  On the fixture no pixel is claimed twice at
+    0.2, 0.1, 0.05 or 0.02602 deg (tests/test_tessellated.py)."""
     labels = np.zeros((n, n), np.int32)
-    for i, ring in enumerate(rings):
-        labels[rasterize_cell(ring, n)] = i + 1
+    for i in (range(len(rings)) if order is None else order):
+        labels[rasterize_cell(rings[i], n)] = i + 1
     empty = labels == 0
     if empty.any():
         iy, ix = np.nonzero(~empty)
