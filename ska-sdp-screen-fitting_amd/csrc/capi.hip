@@ -73,6 +73,11 @@ int sf_create(int device, sf_ctx** out) {
   SF_HIP(hipSetDevice(device));
   sf_ctx* ctx = new sf_ctx();
   ctx->device = device;
+  if (hipMalloc(reinterpret_cast<void**>(&ctx->d_trash), 1024) != hipSuccess) {
+    delete ctx;
+    set_error("sf_create: hipMalloc failed");
+    return SF_ENOMEM;
+  }
   *out = ctx;
   return SF_OK;
 }
@@ -102,6 +107,7 @@ int sf_destroy(sf_ctx* ctx) {
   hipFree(ctx->d_gw);
   hipFree(ctx->d_smooth);
   hipFree(ctx->d_tess_tab);
+  hipFree(ctx->d_trash);
   delete ctx;
   return SF_OK;
 }

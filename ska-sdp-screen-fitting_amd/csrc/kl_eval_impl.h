@@ -66,6 +66,45 @@ __device__ __forceinline__ void sincos_rev(float f, float& s, float& c) {
   c = __builtin_amdgcn_cosf(f);
 }
 
+// The two halves of load_coef, for software pipelining: load_coef_raw
+// issues the KS loads of a group's fragments (clamped addresses, no use of
+// the data), coef_finish applies the scale and zeroes the lanes past S or D
+// once they have landed.  The register tile issues group g + 1's loads before
+// group g's MFMAs, so their L2 round trip hides behind a whole group of MFMA
+// and epilogue work instead of stalling the wave at the top of every group
+// (vmcnt counts loads and stores in issue order: waiting for loads issued
+// before group g's stores does not wait for the stores).
+template <int KS>
+__device__ __forceinline__ void load_coef_raw(double (&v)[KS],
+                                              const double* __restrict__ coef,
+                                              int64_t s0, int64_t S, int D, int l) {
+  const int64_t s = s0 + (l & 15);
+  const double* row = coef + (s < S ? s : S - 1) * D;
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) {
+    const int d = 4 * kk + (l >> 4);
+    v[kk] = row[d < D ? d : D - 1];
+  }
+}
+
+// select without a branch: an all-ones / all-zeros mask on the bits (the
+// compiler turns a plain `ok ? x : 0.0` over a whole fragment into an
+// exec-masked region with its own load waits)
+__device__ __forceinline__ double keep_if(bool ok, double x) {
+  const unsigned long long m = ok ? ~0ull : 0ull;
+  return __builtin_bit_cast(double, __builtin_bit_cast(unsigned long long, x) & m);
+}
+
+template <int KS>
+__device__ __forceinline__ void coef_finish(double (&af)[KS], const double (&v)[KS],
+                                            int64_t s0, int64_t S, int D, int l,
+                                            double scale) {
+  const bool srow = s0 + (l & 15) < S;
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk)
+    af[kk] = keep_if(srow && 4 * kk + (l >> 4) < D, v[kk] * scale);
+}
+
 // MFMA A fragments of a 16-slot group: lane l holds coef[s0 + (l & 15)]
 // [4 kk + (l >> 4)] for every k-step (0 past S or D), times `scale`.  The
 // loads are unconditional (clamped addresses, then a select), so all KS of
@@ -257,14 +296,19 @@ __device__ __forceinline__ float amp2f(double log2a) {
 // wave, and take its 16-slot groups round-robin -- the register tile at
 // ~half the VGPRs, so large D (config 5: D = 50) runs 4 waves per SIMD
 // without spilling; same MFMA operands in the same order, same bits.
+// BEM: byte order of the stores -- 0 little-endian, 1 big-endian (FITS),
+// 2 chosen per launch from SF_EVAL_BIG_ENDIAN (a branch around two copies of
+// the epilogue; the hot float4 / fast-sincos variants are compiled per byte
+// order instead: with the branch the compiler's wait for the next group's
+// coefficient loads also waits for most of this group's stores)
 template <int KS, int MINW, bool VEC4, bool FAST, bool NT, bool GAIN,
-          bool SHB = false>
+          bool SHB = false, int BEM = 2>
 __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
     const double* __restrict__ cfrag, const double* __restrict__ coef,
     const double* __restrict__ coef_xx, const double* __restrict__ coef_yy,
     int D, int64_t S, int64_t P, int64_t n_pb, int64_t n_sc, int chunk_groups,
     float* __restrict__ out, int64_t ring, int64_t ring_base, unsigned flags,
-    unsigned* __restrict__ sums) {
+    unsigned* __restrict__ sums, float* __restrict__ trash) {
   constexpr int kFrag = KS * kTiles * 64;  // Cpix doubles of a wave pixel block
   __shared__ double bsh[SHB ? kFrag : 1];
   const int l = threadIdx.x & 63;
@@ -319,19 +363,47 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
       pslot = ~0u;
       gq = 0;
     };
-    for (int g = SHB ? w : 0; g < chunk_groups; g += SHB ? kEvalWaves : 1) {
+    // coefficient fragments, loaded one group ahead: the raw loads of group
+    // g + 1 go out before group g's MFMAs and stores (load_coef_raw) and are
+    // finished (scaled, masked) at the end of group g; gain: the XX / YY
+    // loads go out with the phase ones
+    constexpr int kGStep = SHB ? kEvalWaves : 1;
+    const double sx = FAST ? kLog2of10 : 1.0;
+    double rf[KS], rx[GAIN ? KS : 1], ry[GAIN ? KS : 1];
+    double af[KS], ax[GAIN ? KS : 1], ay[GAIN ? KS : 1];
+    {
+      const int64_t s0 = slot_base + (SHB ? w : 0) * 16;
+      load_coef_raw<KS>(rf, coef, s0, S, D, l);
+      coef_finish<KS>(af, rf, s0, S, D, l, kInv2Pi);  // phase in turns
+      if constexpr (GAIN) {
+        load_coef_raw<KS>(rx, coef_xx, s0, S, D, l);
+        load_coef_raw<KS>(ry, coef_yy, s0, S, D, l);
+        coef_finish<KS>(ax, rx, s0, S, D, l, sx);
+        coef_finish<KS>(ay, ry, s0, S, D, l, sx);
+      }
+      // the Cpix fragments too must have landed before the group loop: else
+      // the compiler, merging this path with the loop's back edge, waits for
+      // them inside the loop with a count that covers the previous group's
+      // stores as well
+      if constexpr (!SHB) {
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+          for (int t = 0; t < kTiles; ++t) asm volatile("" ::"v"(bf[kk][t]));
+      }
+    }
+    for (int g = SHB ? w : 0; g < chunk_groups; g += kGStep) {
       const int64_t s0 = slot_base + (int64_t)g * 16;
       if (s0 >= S) break;
       // SHB: keep the Cpix reads inside the loop (in LDS, not hoisted into
       // registers, which is the point)
       if constexpr (SHB) asm volatile("" ::: "memory");
-      double af[KS];
-      load_coef<KS>(af, coef, s0, S, D, l, kInv2Pi);  // phase in turns
-      // gain: the XX / YY coefficient loads go out with the phase ones
-      double ax[GAIN ? KS : 1], ay[GAIN ? KS : 1];
+      // the next group's loads (a clamped dummy past the chunk or S)
+      const int64_t s1 = s0 + 16 * kGStep;
+      load_coef_raw<KS>(rf, coef, s1, S, D, l);
       if constexpr (GAIN) {
-        load_coef<KS>(ax, coef_xx, s0, S, D, l, FAST ? kLog2of10 : 1.0);
-        load_coef<KS>(ay, coef_yy, s0, S, D, l, FAST ? kLog2of10 : 1.0);
+        load_coef_raw<KS>(rx, coef_xx, s1, S, D, l);
+        load_coef_raw<KS>(ry, coef_yy, s1, S, D, l);
       }
       // ring slot of the group's first slot (S, ring < 2^31: launch_eval);
       // the 16 rows follow it with at most one wrap when the ring is >= 16
@@ -370,7 +442,13 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
         constexpr bool kBE = decltype(be_tag)::value;
         const int row = acc_row(l, r);
         const int64_t s = s0 + row;
-        if (s >= S) return;  // uniform over the 16 lanes of a slot row
+        // float4 path: rows past S and the float4s past P store into the
+        // context's trash block instead of branching round the stores, so
+        // every path through the epilogue issues the same 16 stores and the
+        // compiler can wait for the next group's coefficient loads with
+        // vmcnt(16) instead of vmcnt(0) (i.e. for this group's stores too)
+        const bool live = s < S && (!VEC4 || p0 < P);
+        if (!VEC4 && s >= S) return;  // uniform over the 16 lanes of a slot row
         uint32_t so = ring0 + (uint32_t)row;
         if (ring >= 16) {
           if (so >= (uint32_t)ring) so -= (uint32_t)ring;
@@ -442,27 +520,28 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
 #pragma unroll
             for (int q = 0; q < 4; ++q) pv[q][t] = bswapf(pv[q][t]);
         }
-        float* o = out + ((int64_t)so * 4) * P + p0;
         unsigned cs = 0u;
         if (VEC4) {
           // P % 4 == 0: a lane's 4 pixels are all inside the grid or all out
           // (the last wave block of a grid that is not a multiple of 64)
-          if (p0 < P) {
+          float* o = live ? out + ((int64_t)so * 4) * P + p0 : trash + 4 * l;
+          const int64_t qstride = live ? P : 0;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const v4f v = {pv[q][0], pv[q][1], pv[q][2], pv[q][3]};
-              store4<NT>(o + q * P, v);
-            }
-            if (sums) {
-              // phase screens store (cos, sin) twice: sum the planes once
-              // (the flush doubles the total)
+          for (int q = 0; q < 4; ++q) {
+            const v4f v = {pv[q][0], pv[q][1], pv[q][2], pv[q][3]};
+            store4<NT>(o + q * qstride, v);
+          }
+          if (sums) {
+            // phase screens store (cos, sin) twice: sum the planes once
+            // (the flush doubles the total)
 #pragma unroll
-              for (int q = 0; q < (GAIN ? 4 : 2); ++q)
+            for (int q = 0; q < (GAIN ? 4 : 2); ++q)
 #pragma unroll
-                for (int t = 0; t < kTiles; ++t) cs += fbits(pv[q][t]);
-            }
+              for (int t = 0; t < kTiles; ++t) cs += fbits(pv[q][t]);
+            cs = live ? cs : 0u;
           }
         } else {
+          float* o = out + ((int64_t)so * 4) * P + p0;
 #pragma unroll
           for (int t = 0; t < kTiles; ++t) {
             if (p0 + t < P) {
@@ -476,7 +555,13 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
         }
         if (sums) part[r] = cs;  // the 16 lanes of the row sum it below
       };
-      if (be) {
+      if constexpr (BEM == 1) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) row_out(r, std::true_type{});
+      } else if constexpr (BEM == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) row_out(r, std::false_type{});
+      } else if (be) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) row_out(r, std::true_type{});
       } else {
@@ -490,6 +575,11 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
           pslot = (uint32_t)(s0 + 4 * ((l >> 2) & 3) + (l >> 4));
         }
         if (++gq == 4) flush_sums();
+      }
+      coef_finish<KS>(af, rf, s1, S, D, l, kInv2Pi);
+      if constexpr (GAIN) {
+        coef_finish<KS>(ax, rx, s1, S, D, l, sx);
+        coef_finish<KS>(ay, ry, s1, S, D, l, sx);
       }
     }
     if (sums) flush_sums();
@@ -753,10 +843,13 @@ int launch_eval_ks(sf_ctx* ctx, const double* coef,
   const bool fast = flags & SF_EVAL_FAST_SINCOS;
   const bool nt = flags & SF_EVAL_NT_STORES;
   const bool gain = cxx != nullptr;
-#define SF_LAUNCH(V, F, N, G)                                                 \
-  hipLaunchKernelGGL((kl_eval_kernel<KS, MINW, V, F, N, G>), dim3((unsigned)nblk),  \
-                     dim3(256), 0, ctx->stream, ctx->d_cfrag, cb, cxb, cyb, \
-                     ctx->D, S, P, n_pb, n_sc, groups, out, ring, b % ring, fl, sb)
+  const bool be = flags & SF_EVAL_BIG_ENDIAN;
+#define SF_LAUNCH_B(V, F, N, G, B)                                              \
+  hipLaunchKernelGGL((kl_eval_kernel<KS, MINW, V, F, N, G, false, B>),          \
+                     dim3((unsigned)nblk), dim3(256), 0, ctx->stream,           \
+                     ctx->d_cfrag, cb, cxb, cyb, ctx->D, S, P, n_pb, n_sc,      \
+                     groups, out, ring, b % ring, fl, sb, ctx->d_trash)
+#define SF_LAUNCH(V, F, N, G) SF_LAUNCH_B(V, F, N, G, 2)
 #define SF_LAUNCH_G(V, F, N) \
   do {                       \
     if (gain)                \
@@ -764,17 +857,30 @@ int launch_eval_ks(sf_ctx* ctx, const double* coef,
     else                     \
       SF_LAUNCH(V, F, N, false); \
   } while (0)
+  // float4 + fast sincos (every hot call): the byte order compiled in
+#define SF_LAUNCH_GB(N)                                  \
+  do {                                                   \
+    if (gain) {                                          \
+      if (be) SF_LAUNCH_B(true, true, N, true, 1);       \
+      else SF_LAUNCH_B(true, true, N, true, 0);          \
+    } else {                                             \
+      if (be) SF_LAUNCH_B(true, true, N, false, 1);      \
+      else SF_LAUNCH_B(true, true, N, false, 0);         \
+    }                                                    \
+  } while (0)
   if (vec4) {
     if (fast) {
-      if (nt) SF_LAUNCH_G(true, true, true); else SF_LAUNCH_G(true, true, false);
+      if (nt) SF_LAUNCH_GB(true); else SF_LAUNCH_GB(false);
     } else {
       if (nt) SF_LAUNCH_G(true, false, true); else SF_LAUNCH_G(true, false, false);
     }
   } else {
     if (fast) SF_LAUNCH_G(false, true, false); else SF_LAUNCH_G(false, false, false);
   }
+#undef SF_LAUNCH_GB
 #undef SF_LAUNCH_G
 #undef SF_LAUNCH
+#undef SF_LAUNCH_B
   SF_HIP(hipGetLastError());
   }
   return SF_OK;
@@ -803,7 +909,7 @@ int launch_eval_shb(sf_ctx* ctx, const double* coef, int64_t S_all,
                      dim3((unsigned)nblk), dim3(256), 0, ctx->stream,           \
                      ctx->d_cfrag, cb, nullptr, nullptr, ctx->D, S, P, n_wpb, \
                      n_sc, groups, out, ring, b % ring,                         \
-                     flags | eval_band_flags(ctx, n_wpb), sb)
+                     flags | eval_band_flags(ctx, n_wpb), sb, ctx->d_trash)
   if (fast) {
     if (nt) SF_LAUNCH_SHB(true, true); else SF_LAUNCH_SHB(true, false);
   } else {

@@ -84,6 +84,7 @@ struct sf_ctx {
   double* d_gw = nullptr;
   size_t gw_cap = 0;                     // doubles
   double gw_sigma = -1.0;                // sigma whose weights d_gw holds
+  float* d_trash = nullptr;  // 1 KiB sink of the eval's out-of-range stores
   float* d_smooth = nullptr;
   size_t smooth_cap = 0;                 // bytes
   float* d_tess_tab = nullptr;           // tessellated value table [S][D+1][4]
