@@ -293,6 +293,7 @@ int sf_set_basis(sf_ctx* ctx, const double* pp, int D, double r0,
   SF_TRY(dev_alloc(&ctx->d_eig, (size_t)64));
   SF_HIP(hipMemcpy(ctx->d_pp, pp, sizeof(double) * 3 * D,
                    hipMemcpyHostToDevice));
+  for (int i = 0; i < 3 * D; ++i) ctx->h_pp[i] = pp[i];
   SF_HIP(hipMemset(ctx->d_eig, 0, 64 * sizeof(double)));
   ctx->D = D;
   ctx->r0 = r0;
@@ -417,7 +418,24 @@ int sf_set_grid(sf_ctx* ctx, const double* x, int nx, const double* y,
   }
   (void)hipFree(dx);
   (void)hipFree(dy);
-  if (rc == SF_OK) ctx->n_pix = n_pix;
+  if (rc == SF_OK) {
+    // largest |Cpix| over the grid (kl_cpix_kernel's formula on the farthest
+    // corner of each direction, 1 % margin for the device pow): the
+    // fixed-point phase epilogue's group bound
+    double cmax = 0.0;
+    for (int d = 0; d < ctx->D; ++d) {
+      double mx = 0.0, my = 0.0;
+      for (int i = 0; i < nx; ++i) mx = std::fmax(mx, std::fabs(ctx->h_pp[3 * d] - x[i]));
+      for (int j = 0; j < ny; ++j) my = std::fmax(my, std::fabs(ctx->h_pp[3 * d + 1] - y[j]));
+      const double z = ctx->h_pp[3 * d + 2];
+      const double d2 = mx * mx + my * my + z * z;
+      cmax = std::fmax(cmax, 0.5 * std::pow(d2 / (ctx->r0 * ctx->r0), ctx->beta / 2.0));
+    }
+    cmax *= 1.01;
+    // per lane (a quarter of a slot's directions): 2^17 / 4 turns
+    ctx->rev_thr = cmax > 0.0 && std::isfinite(cmax) ? 32768.0 / cmax : 0.0;
+    ctx->n_pix = n_pix;
+  }
   return rc;
 }
 

@@ -59,6 +59,61 @@ __device__ __forceinline__ void rev_reduce_n(float (&f)[N], const double (&rev)[
   }
 }
 
+// Fixed-point phase reduction (fast epilogue, round 3).  The phase
+// contraction starts its accumulators at kRevMagic = 1.5 * 2^20 instead of 0,
+// so the fp64 MFMA result is y = M + rev with ulp 2^-32 wherever |rev| <
+// 2^19: the low dword of y is frac(rev) * 2^32 as a two's-complement int,
+// i.e. the phase reduced to [-1/2, 1/2) turn in 32-bit fixed point, already
+// rounded by the accumulation (<= KS * 2^-32 turn).  One v_cvt_f32_i32 and
+// one v_mul_f32 then give the float argument of v_sin / v_cos, where the
+// exact reduction rev - rint(rev) took v_rndne_f64 + v_add_f64 +
+// v_cvt_f32_f64 (4.4 issue cycles each, profiles/round3b_valu_cost.txt):
+// float(lo) * 2^-32 == float(rev' - rint(rev')) for rev' = y - M exactly.
+// A 16-slot group takes this path only when every lane's coefficient sum
+// bounds its phases below 2^17 turns (group_rev_safe: a lane holds a quarter
+// of a slot's directions, so sum |coef| / 2 pi < rev_thr = 2^15 / max |Cpix|
+// per lane) -- which also proves them finite, so no NaN scrub is needed
+// there; any other group (NaN / Inf coefficients, huge phases) takes the
+// exact path on rev' = y - M, NaN / Inf propagating.  The check costs KS
+// fp64 adds per lane and group, about what the fixed point saves per value
+// at D = 50 -- where the fixed point also measured 3-4 % slower in the
+// config-5 bench (profiles/round3m_eval_fixed_point_ab.txt) -- so it is
+// used up to kMagicMaxKS k-steps (D <= 44, the LDS-staged kernels' range),
+// the exact reduction above; every kernel variant of a given D takes the
+// same path and writes the same bits.
+constexpr double kRevMagic = 1572864.0;          // 1.5 * 2^20
+constexpr float kTwoM32 = 2.3283064365386963e-10f;  // 2^-32
+constexpr int kMagicMaxKS = 11;
+
+template <int KS>
+__device__ __forceinline__ bool group_rev_safe(const double (&af)[KS], double thr) {
+  double sum = 0.0;
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) sum += fabs(af[kk]);
+  return __builtin_amdgcn_ballot_w64(!(sum < thr)) == 0;  // NaN: not safe
+}
+
+__device__ __forceinline__ float rev_fixed(double y) {
+  const int lo = (int)(unsigned)__double_as_longlong(y);
+  return (float)lo * kTwoM32;
+}
+
+// rev_reduce_n of magic-started accumulators: fixed point when the group is
+// safe, else the exact reduction of y - M (scrub as rev_reduce_n)
+template <int N>
+__device__ __forceinline__ void rev_reduce_magic(float (&f)[N], const double (&y)[N],
+                                                 bool safe, double a0, bool scrub) {
+  if (safe) {
+#pragma unroll
+    for (int t = 0; t < N; ++t) f[t] = rev_fixed(y[t]);
+  } else {
+    double rv[N];
+#pragma unroll
+    for (int t = 0; t < N; ++t) rv[t] = y[t] - a0;
+    rev_reduce_n<N>(f, rv, scrub);
+  }
+}
+
 // v_sin_f32 / v_cos_f32 return NaN for a NaN argument (checked by the
 // unscrubbed cases of tests/test_gpu_parity.py::test_eval_kernels_agree)
 __device__ __forceinline__ void sincos_rev(float f, float& s, float& c) {
@@ -308,8 +363,10 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
     const double* __restrict__ coef_xx, const double* __restrict__ coef_yy,
     int D, int64_t S, int64_t P, int64_t n_pb, int64_t n_sc, int chunk_groups,
     float* __restrict__ out, int64_t ring, int64_t ring_base, unsigned flags,
-    unsigned* __restrict__ sums, float* __restrict__ trash) {
+    unsigned* __restrict__ sums, float* __restrict__ trash, double rev_thr) {
   constexpr int kFrag = KS * kTiles * 64;  // Cpix doubles of a wave pixel block
+  // fixed-point phase reduction (kRevMagic) for D <= 44
+  constexpr bool kMagic = FAST && KS <= kMagicMaxKS;
   __shared__ double bsh[SHB ? kFrag : 1];
   const int l = threadIdx.x & 63;
   // wave index, wave-uniform: keeps slot / ring arithmetic on the SALU
@@ -371,10 +428,12 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
     const double sx = FAST ? kLog2of10 : 1.0;
     double rf[KS], rx[GAIN ? KS : 1], ry[GAIN ? KS : 1];
     double af[KS], ax[GAIN ? KS : 1], ay[GAIN ? KS : 1];
+    bool safe = false;
     {
       const int64_t s0 = slot_base + (SHB ? w : 0) * 16;
       load_coef_raw<KS>(rf, coef, s0, S, D, l);
       coef_finish<KS>(af, rf, s0, S, D, l, kInv2Pi);  // phase in turns
+      if constexpr (kMagic) safe = group_rev_safe<KS>(af, rev_thr);
       if constexpr (GAIN) {
         load_coef_raw<KS>(rx, coef_xx, s0, S, D, l);
         load_coef_raw<KS>(ry, coef_yy, s0, S, D, l);
@@ -409,9 +468,11 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
       // the 16 rows follow it with at most one wrap when the ring is >= 16
       // slots -- scalar, no per-lane 64-bit modulo
       const uint32_t ring0 = (uint32_t)(s0 + ring_base) % (uint32_t)ring;
+      // fast epilogue: fixed-point phase accumulators (kRevMagic)
+      const double a0 = kMagic ? kRevMagic : 0.0;
       v4d acc[kTiles];
 #pragma unroll
-      for (int t = 0; t < kTiles; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
+      for (int t = 0; t < kTiles; ++t) acc[t] = v4d{a0, a0, a0, a0};
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
@@ -433,6 +494,27 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
             accx[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ax[kk], bval(kk, t), accx[t], 0, 0, 0);
             accy[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ay[kk], bval(kk, t), accy[t], 0, 0, 0);
           }
+      }
+      // fast epilogue: the reduced phases of the group's 4 x 4 values, fixed
+      // point or exact by ONE wave-uniform branch per group (per-row
+      // branches measured 4 % slower at D = 50); gain screens scrub the
+      // products, phase screens the reduced argument (cos 1, sin 0)
+      float frg[4][kTiles];
+      if constexpr (FAST) {
+        if (safe) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int t = 0; t < kTiles; ++t) frg[r][t] = rev_fixed(acc[t][r]);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            double rv[kTiles];
+#pragma unroll
+            for (int t = 0; t < kTiles; ++t) rv[t] = acc[t][r] - a0;
+            rev_reduce_n<kTiles>(frg[r], rv, !GAIN && scrub);
+          }
+        }
       }
       // this lane's checksum partial of each of its 4 slot rows
       unsigned part[4] = {0u, 0u, 0u, 0u};
@@ -463,22 +545,18 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
         // the wave has a NaN (a wave-uniform branch; same bits either way)
         constexpr bool kScrubValues = GAIN || !FAST;
         bool bad = false;
-        // phase screens, fast epilogue: the reduced arguments of the 4 tiles
-        // first, NaN scrubbed together (cos 1, sin 0)
-        float fr[kTiles];
-        if constexpr (FAST && !GAIN) {
-          double rv[kTiles];
-#pragma unroll
-          for (int t = 0; t < kTiles; ++t) rv[t] = acc[t][r];
-          rev_reduce_n<kTiles>(fr, rv, scrub);
-        }
+        // fast epilogue: this row's reduced arguments (frg, above)
+        const float(&fr)[kTiles] = frg[r];
 #pragma unroll
         for (int t = 0; t < kTiles; ++t) {
           float sf, cf;
           if (GAIN) {
             // a NaN phase stays NaN through A * cos and is scrubbed below,
             // as the reference scrubs the product (screen.py:368-378)
-            jones_sincos<FAST>(acc[t][r], sf, cf, false);
+            if (FAST)
+              sincos_rev(fr[t], sf, cf);
+            else
+              jones_sincos<false>(acc[t][r], sf, cf, false);
             if (FAST) {
               // fp32 amplitude x fp32 cos / sin: within 2e-6 x max(1, A)
               const float ax = amp2f(accx[t][r]);
@@ -577,6 +655,7 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
         if (++gq == 4) flush_sums();
       }
       coef_finish<KS>(af, rf, s1, S, D, l, kInv2Pi);
+      if constexpr (kMagic) safe = group_rev_safe<KS>(af, rev_thr);
       if constexpr (GAIN) {
         coef_finish<KS>(ax, rx, s1, S, D, l, sx);
         coef_finish<KS>(ay, ry, s1, S, D, l, sx);
@@ -615,7 +694,7 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
     int ks_real, int64_t S, int64_t P, int64_t n_pb, int64_t n_sc,
     int chunk_groups, float* __restrict__ out, int64_t ring, int64_t ring_base,
     unsigned flags,
-    int sleep, unsigned* __restrict__ sums) {
+    int sleep, unsigned* __restrict__ sums, double rev_thr) {
   using L = EvalLds<NW, TPW>;
   __shared__ float tile[2][16][L::kStride];
   // checksums: slot sums of up to 16 groups per half ([half][group % 16]
@@ -667,9 +746,15 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
       // ---- contraction: 16 slots x this wave's 64 pixels
       double af[KS];
       load_coef<KS>(af, coef, s0, S, D, l, kInv2Pi);
+      // fixed-point phase accumulators (kRevMagic) while the REAL k-step
+      // count (ks_real: KS may be zero-padded) is in the fixed-point range,
+      // as the register tile of the same D
+      const bool magic = ks_real <= kMagicMaxKS;
+      const double a0 = magic ? kRevMagic : 0.0;
+      const bool safe = magic && group_rev_safe<KS>(af, rev_thr);
       v4d acc[TPW];
 #pragma unroll
-      for (int t = 0; t < TPW; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
+      for (int t = 0; t < TPW; ++t) acc[t] = v4d{a0, a0, a0, a0};
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
@@ -682,7 +767,7 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
         double rv[TPW];
 #pragma unroll
         for (int t = 0; t < TPW; ++t) rv[t] = acc[t][r];
-        rev_reduce_n<TPW>(red, rv, scrub);
+        rev_reduce_magic<TPW>(red, rv, safe, a0, scrub);
         float* dst = &buf[acc_row(l, r)][wblk * kWavePix + (l & 15) * kTiles + t0];
         if (TPW == 4)
           *reinterpret_cast<v4f*>(dst) = v4f{red[0], red[1], red[2 % TPW], red[3 % TPW]};
@@ -848,7 +933,8 @@ int launch_eval_ks(sf_ctx* ctx, const double* coef,
   hipLaunchKernelGGL((kl_eval_kernel<KS, MINW, V, F, N, G, false, B>),          \
                      dim3((unsigned)nblk), dim3(256), 0, ctx->stream,           \
                      ctx->d_cfrag, cb, cxb, cyb, ctx->D, S, P, n_pb, n_sc,      \
-                     groups, out, ring, b % ring, fl, sb, ctx->d_trash)
+                     groups, out, ring, b % ring, fl, sb, ctx->d_trash,        \
+                     ctx->rev_thr)
 #define SF_LAUNCH(V, F, N, G) SF_LAUNCH_B(V, F, N, G, 2)
 #define SF_LAUNCH_G(V, F, N) \
   do {                       \
@@ -909,7 +995,8 @@ int launch_eval_shb(sf_ctx* ctx, const double* coef, int64_t S_all,
                      dim3((unsigned)nblk), dim3(256), 0, ctx->stream,           \
                      ctx->d_cfrag, cb, nullptr, nullptr, ctx->D, S, P, n_wpb, \
                      n_sc, groups, out, ring, b % ring,                         \
-                     flags | eval_band_flags(ctx, n_wpb), sb, ctx->d_trash)
+                     flags | eval_band_flags(ctx, n_wpb), sb, ctx->d_trash,     \
+                     ctx->rev_thr)
   if (fast) {
     if (nt) SF_LAUNCH_SHB(true, true); else SF_LAUNCH_SHB(true, false);
   } else {
@@ -957,12 +1044,12 @@ int launch_eval_lds(sf_ctx* ctx, const double* coef, int64_t S_all,
     hipLaunchKernelGGL((kl_eval_lds_kernel<KS, NW, TPW, true>), dim3((unsigned)nblk),
                        dim3(64 * NW), 0, ctx->stream, ctx->d_cfrag, cb, ctx->D,
                        ctx->ksteps, S, P, n_pb, n_sc, groups, out, ring, b % ring,
-                       fl, ctx->eval_sleep, sb);
+                       fl, ctx->eval_sleep, sb, ctx->rev_thr);
   else
     hipLaunchKernelGGL((kl_eval_lds_kernel<KS, NW, TPW, false>), dim3((unsigned)nblk),
                        dim3(64 * NW), 0, ctx->stream, ctx->d_cfrag, cb, ctx->D,
                        ctx->ksteps, S, P, n_pb, n_sc, groups, out, ring, b % ring,
-                       fl, ctx->eval_sleep, sb);
+                       fl, ctx->eval_sleep, sb, ctx->rev_thr);
   SF_HIP(hipGetLastError());
   }
   return SF_OK;

@@ -56,6 +56,10 @@ struct sf_ctx {
   int64_t n_pix_blocks = 0;    // workgroup pixel blocks (kBlockPix)
   int ksteps = 0;              // ceil(D / 4)
   double* d_cfrag = nullptr;   // [wave pixel blocks][ksteps][kTiles][64]
+  // fixed-point phase epilogue: a lane's |coef| sum (turns) below rev_thr
+  // bounds its phases below 2^17 turns (kl_eval_impl.h group_rev_safe)
+  double rev_thr = 0.0;
+  double h_pp[3 * SF_MAX_DIR] = {};  // host copy of the piercepoints
   // fit scratch
   uint8_t* d_skip = nullptr;   // [F][A] block skip flags
   size_t skip_cap = 0;
