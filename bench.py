@@ -108,6 +108,9 @@ def parse():
     ap.add_argument("--tess-waves", type=int, default=0,
                     help="SF_OPT_TESS_WAVES: waves per workgroup of the "
                          "unsmoothed tessellated fill (0 = library default)")
+    ap.add_argument("--tess-box", type=int, default=-1, choices=(-1, 0, 1),
+                    help="SF_OPT_TESS_BOX: smoothed tessellated fill by interior "
+                         "lookups (1), by the wide-tile kernel (0) or auto (-1)")
     ap.add_argument("--tess-gain", action="store_true",
                     help="--screen tess: XX / YY amplitudes too (four "
                          "distinct planes, A cos / A sin)")
@@ -555,8 +558,8 @@ def tess_steps(args, ctx, torch, dev, dist, world, rank, coll_dev, sol, setup,
     referenced per-direction cos / sin by the Voronoi label raster, optional
     fused Gaussian) of every slot of the rank into the HBM ring; the label
     template is built once on the host (voronoi_screen.py:218-351)."""
-    from ska_sdp_screen_fitting_amd._lib import (SF_EVAL_NAN_SCRUB, SF_OPT_TESS_SLOTS,
-                                                 SF_OPT_TESS_WAVES)
+    from ska_sdp_screen_fitting_amd._lib import (SF_EVAL_NAN_SCRUB, SF_OPT_TESS_BOX,
+                                                 SF_OPT_TESS_SLOTS, SF_OPT_TESS_WAVES)
     from ska_sdp_screen_fitting_amd.synthetic import (FIELD_DEC_DEG,
                                                       FIELD_RA_DEG,
                                                       FIELD_WIDTH_DEG)
@@ -579,6 +582,7 @@ def tess_steps(args, ctx, torch, dev, dist, world, rank, coll_dev, sol, setup,
         ctx.set_option(SF_OPT_TESS_SLOTS, args.tess_slots)
     if args.tess_waves:
         ctx.set_option(SF_OPT_TESS_WAVES, args.tess_waves)
+    ctx.set_option(SF_OPT_TESS_BOX, args.tess_box)
     flags = SF_EVAL_NAN_SCRUB
 
     amp = {}
@@ -643,8 +647,12 @@ def tess_steps(args, ctx, torch, dev, dist, world, rank, coll_dev, sol, setup,
     if rank == 0:
         bytes_launch = S * (16 * P + 8 * D)
         achieved = bytes_launch / launch_s / 1e9
-        kernel = ("kl_tess_gather_kernel" if args.smooth_pix == 0
-                  else "kl_tess_smooth_kernel")
+        # the library's choice (tess.hip launch_tess, SF_OPT_TESS_BOX auto)
+        R = int(4.0 * args.smooth_pix + 0.5) if args.smooth_pix > 0 else 0
+        box = 0 < R <= 24 and (args.tess_box == 1 or (args.tess_box < 0 and
+                                                       args.tess_gain and R <= 2))
+        kernel = ("kl_tess_gather_kernel" if R == 0 else
+                  "kl_tess_box_kernel" if box else "kl_tess_smooth_kernel")
         # PMC traffic (profiles/traffic.json) when measured on this call shape
         traffic = None
         wkey = (args.workload + "-tess" + ("-gain" if args.tess_gain else "")

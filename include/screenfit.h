@@ -160,6 +160,13 @@ int sf_device_cus(sf_ctx* ctx, int* n_cu);
  * 16 x 16 tile kernel instead of the table + gather / wide-tile smoothing
  * kernels (same bits; for cross-checks). */
 #define SF_OPT_TESS_TILE 13
+/* SF_OPT_TESS_BOX = 1: sf_tess_fill with smoothing (radius <= 24) stores
+ * the pixels whose whole (2R + 1)^2 neighbourhood is one cell from a
+ * per-(slot, cell) value and sums only the others (kl_tess_box_kernel); 0:
+ * the wide-tile kernel that sums every pixel; -1 (default): the first for
+ * four planes (XX / YY amplitudes) at radius <= 2, else the second.  Same
+ * bits. */
+#define SF_OPT_TESS_BOX 14
 #define SF_EVAL_KERNEL_AUTO 0
 #define SF_EVAL_KERNEL_TILE 1
 #define SF_EVAL_KERNEL_LDS4 2

@@ -208,6 +208,11 @@ int sf_set_option(sf_ctx* ctx, int option, int value) {
       SF_REQUIRE(value == 0 || value == 1, SF_EINVAL, "sf_set_option: tess tile must be 0 or 1");
       ctx->tess_tile = value;
       return SF_OK;
+    case SF_OPT_TESS_BOX:
+      SF_REQUIRE(value >= -1 && value <= 1, SF_EINVAL,
+                 "sf_set_option: tess box must be -1, 0 or 1");
+      ctx->tess_box = value;
+      return SF_OK;
     case SF_OPT_TESS_WAVES:
       SF_REQUIRE(value == 0 || value == 4 || value == 8 || value == 16, SF_EINVAL,
                  "sf_set_option: tess waves must be 0, 4, 8 or 16");

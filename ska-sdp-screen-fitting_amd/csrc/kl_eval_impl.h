@@ -356,8 +356,14 @@ __device__ __forceinline__ float amp2f(double log2a) {
 // the epilogue; the hot float4 / fast-sincos variants are compiled per byte
 // order instead: with the branch the compiler's wait for the next group's
 // coefficient loads also waits for most of this group's stores)
+// DIRECT: every group of the launch is 16 live slots that do not wrap round
+// the ring, in 64-pixel blocks inside the grid (launch_eval_ks sends a ragged
+// tail to the general kernel): lane row (l >> 4) + 4 r of a group stores to
+// lane_base + 16 r P -- one base per group instead of, per row, a ring index,
+// a 64-bit product and the trash select (a run-time choice between the two
+// would again be a branch round the stores, see BEM)
 template <int KS, int MINW, bool VEC4, bool FAST, bool NT, bool GAIN,
-          bool SHB = false, int BEM = 2>
+          bool SHB = false, int BEM = 2, bool DIRECT = false>
 __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
     const double* __restrict__ cfrag, const double* __restrict__ coef,
     const double* __restrict__ coef_xx, const double* __restrict__ coef_yy,
@@ -520,8 +526,11 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
       unsigned part[4] = {0u, 0u, 0u, 0u};
       // one MFMA accumulator row: 4 slot rows x this lane's 4 pixels; BE
       // (FITS byte order) as a compile-time branch of the whole row
+      // DIRECT: the lane's row base of this group (see the template notes)
+      float* const lane_base = out + ((int64_t)(ring0 + (uint32_t)(l >> 4)) * 4) * P + p0;
       auto row_out = [&](int r, auto be_tag) {
         constexpr bool kBE = decltype(be_tag)::value;
+        constexpr bool kDirect = VEC4 && DIRECT;
         const int row = acc_row(l, r);
         const int64_t s = s0 + row;
         // float4 path: rows past S and the float4s past P store into the
@@ -602,8 +611,14 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
         if (VEC4) {
           // P % 4 == 0: a lane's 4 pixels are all inside the grid or all out
           // (the last wave block of a grid that is not a multiple of 64)
-          float* o = live ? out + ((int64_t)so * 4) * P + p0 : trash + 4 * l;
-          const int64_t qstride = live ? P : 0;
+          float* o;
+          int64_t qstride = P;
+          if constexpr (kDirect) {
+            o = lane_base + (int64_t)(16 * r) * P;
+          } else {
+            o = live ? out + ((int64_t)so * 4) * P + p0 : trash + 4 * l;
+            qstride = live ? P : 0;
+          }
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const v4f v = {pv[q][0], pv[q][1], pv[q][2], pv[q][3]};
@@ -616,7 +631,7 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
             for (int q = 0; q < (GAIN ? 4 : 2); ++q)
 #pragma unroll
               for (int t = 0; t < kTiles; ++t) cs += fbits(pv[q][t]);
-            cs = live ? cs : 0u;
+            if constexpr (!kDirect) cs = live ? cs : 0u;
           }
         } else {
           float* o = out + ((int64_t)so * 4) * P + p0;
@@ -633,18 +648,18 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
         }
         if (sums) part[r] = cs;  // the 16 lanes of the row sum it below
       };
+      auto rows_out = [&](auto be_tag) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) row_out(r, be_tag);
+      };
       if constexpr (BEM == 1) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) row_out(r, std::true_type{});
+        rows_out(std::true_type{});
       } else if constexpr (BEM == 0) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) row_out(r, std::false_type{});
+        rows_out(std::false_type{});
       } else if (be) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) row_out(r, std::true_type{});
+        rows_out(std::true_type{});
       } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) row_out(r, std::false_type{});
+        rows_out(std::false_type{});
       }
       if (sums) {
         const unsigned tot = row_sum16_x4(part, l & 15);
@@ -929,13 +944,39 @@ int launch_eval_ks(sf_ctx* ctx, const double* coef,
   const bool nt = flags & SF_EVAL_NT_STORES;
   const bool gain = cxx != nullptr;
   const bool be = flags & SF_EVAL_BIG_ENDIAN;
+  // float4 + fast sincos, 64-pixel blocks inside the grid and a ring of
+  // whole 16-slot groups: the direct-addressing kernel over the whole groups
+  // of the launch, the general one over a ragged tail (< 16 slots)
+  // (up to D = 44: at D = 50 it measured 2 % slower, like the fixed-point
+  // reduction -- profiles/round3o_eval_direct_ab.txt)
+  const bool direct = KS <= kMagicMaxKS && vec4 && fast && P % kWavePix == 0 &&
+                      ring % 16 == 0 && (b % ring) % 16 == 0;
+  const int64_t S_dir = direct ? (S & ~(int64_t)15) : 0;
+#define SF_LAUNCH_BD(V, F, N, G, B, DIR, SL, NSC, NBLK, OFF)                   \
+  hipLaunchKernelGGL((kl_eval_kernel<KS, MINW, V, F, N, G, false, B, DIR>),     \
+                     dim3((unsigned)(NBLK)), dim3(256), 0, ctx->stream,         \
+                     ctx->d_cfrag, cb + (OFF) * ctx->D,                        \
+                     cxb ? cxb + (OFF) * ctx->D : nullptr,                     \
+                     cyb ? cyb + (OFF) * ctx->D : nullptr, ctx->D, SL, P, n_pb, \
+                     NSC, groups, out, ring, (b + (OFF)) % ring, fl,           \
+                     sb ? sb + (OFF) : nullptr, ctx->d_trash, ctx->rev_thr)
 #define SF_LAUNCH_B(V, F, N, G, B)                                              \
-  hipLaunchKernelGGL((kl_eval_kernel<KS, MINW, V, F, N, G, false, B>),          \
-                     dim3((unsigned)nblk), dim3(256), 0, ctx->stream,           \
-                     ctx->d_cfrag, cb, cxb, cyb, ctx->D, S, P, n_pb, n_sc,      \
-                     groups, out, ring, b % ring, fl, sb, ctx->d_trash,        \
-                     ctx->rev_thr)
-#define SF_LAUNCH(V, F, N, G) SF_LAUNCH_B(V, F, N, G, 2)
+  do {                                                                          \
+    if constexpr (KS <= kMagicMaxKS) {                                          \
+      if (S_dir > 0) {                                                          \
+        const int64_t nsc_d = (S_dir + 16 * groups - 1) / (16 * groups);        \
+        SF_LAUNCH_BD(V, F, N, G, B, true, S_dir, nsc_d,                        \
+                     eval_grid(ctx, n_pb, nsc_d, 256), (int64_t)0);            \
+      }                                                                         \
+    }                                                                           \
+    if (S > S_dir) {                                                            \
+      const int64_t nsc_t = (S - S_dir + 16 * groups - 1) / (16 * groups);      \
+      SF_LAUNCH_BD(V, F, N, G, B, false, S - S_dir, nsc_t,                     \
+                   eval_grid(ctx, n_pb, nsc_t, 256), S_dir);                   \
+    }                                                                           \
+  } while (0)
+#define SF_LAUNCH(V, F, N, G) \
+  SF_LAUNCH_BD(V, F, N, G, 2, false, S, n_sc, nblk, (int64_t)0)
 #define SF_LAUNCH_G(V, F, N) \
   do {                       \
     if (gain)                \
@@ -967,6 +1008,7 @@ int launch_eval_ks(sf_ctx* ctx, const double* coef,
 #undef SF_LAUNCH_G
 #undef SF_LAUNCH
 #undef SF_LAUNCH_B
+#undef SF_LAUNCH_BD
   SF_HIP(hipGetLastError());
   }
   return SF_OK;

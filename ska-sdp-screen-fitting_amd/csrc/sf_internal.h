@@ -106,6 +106,7 @@ struct sf_ctx {
   int tess_slots = 0;           // SF_OPT_TESS_SLOTS (0 = auto = 16)
   int tess_waves = 0;           // SF_OPT_TESS_WAVES (0 = auto = 16)
   int tess_tile = 0;            // SF_OPT_TESS_TILE (1: round-1 fused tile kernel)
+  int tess_box = -1;            // SF_OPT_TESS_BOX (-1 auto, 0 wide-tile, 1 interior lookups)
   int fit_pack = 1;             // SF_OPT_FIT_PACK: 2 slots per wave for D <= 32
   int fit_lean = 1;             // SF_OPT_FIT_LEAN: lean pass when weights are uniform
 };

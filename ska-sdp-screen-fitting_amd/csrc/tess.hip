@@ -429,6 +429,214 @@ __global__ __launch_bounds__(256) void kl_tess_smooth_kernel(
   }
 }
 
+// Smoothed fill with interior lookups (round 3; kl_tess_box_kernel).  The
+// unsmoothed image of a slot is piecewise constant: every pixel holds one of
+// the D + 1 table values, chosen by the label raster, which is the same for
+// every slot.  Where the whole (2R + 1)^2 box around a pixel carries one
+// label L, both passes of the Gaussian see 2R + 1 equal inputs, so the
+// pixel's smoothed value is a function of the table entry alone: computed
+// once per (slot, entry) with scipy's arithmetic in scipy's order (y sum of
+// equal doubles -> float -> x sum of equal doubles -> float -> scrub -> swap)
+// it is bit for bit what the full two-pass sum gives there.  Per tile the
+// kernel finds (once, for all the item's slots) the vertically uniform
+// y-pass windows (vlab) and the box-uniform pixels (plab), and lists the
+// others; per slot it then runs the y pass only over the listed windows, the
+// x pass only over the listed (boundary) pixels -- reading a uniform
+// window's y value from the per-entry table -- and stores every pixel from
+// either the per-entry final value or the boundary result.  At sigma 0.5 px
+// (R = 2) about a fifth of a 256^2 Voronoi raster of 20 cells is boundary,
+// so the fp64 VALU work of the passes (3 ops per tap per plane, scipy's
+// order: the reason kl_tess_smooth_kernel is VALU-bound) shrinks ~5x and the
+// fill approaches the gather kernel's store rate.  Same bits as
+// kl_tess_smooth_kernel and kl_tess_kernel.
+constexpr int kBoxTH = 4;       // tile rows (one per wave)
+constexpr int kBoxSlots = 32;   // slots per work item (the tile setup amortises over them)
+constexpr int kBoxMaxR = 24;
+
+template <int RT, int NP>
+__global__ __launch_bounds__(256) void kl_tess_box_kernel(
+    const int32_t* __restrict__ labels, int nx, int ny,
+    const tess_v4f* __restrict__ tab, int D, int64_t S,
+    float* __restrict__ out, int64_t ring, int64_t ring_base,
+    const double* __restrict__ gw, int R_arg, int64_t n_tiles, int64_t n_sc,
+    unsigned flags) {
+#pragma clang fp contract(off)
+  typedef double vacc_t __attribute__((ext_vector_type(NP)));
+  typedef float vyf_t __attribute__((ext_vector_type(NP)));
+  auto widen = [](const auto& v) {
+    vacc_t r;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) r[p] = (double)v[p];
+    return r;
+  };
+  constexpr int kR = RT > 0 ? RT : kBoxMaxR;  // LDS sizing
+  constexpr int kW2 = kSmTW + 2 * kR;
+  constexpr unsigned char kMixed = 0xFF;       // D <= 64 < 0xFF
+  constexpr int kTapUnroll = RT > 0 ? RT : 4;
+  const int R = RT > 0 ? RT : R_arg;
+  const int W2 = kSmTW + 2 * R;
+  const int H2 = kBoxTH + 2 * R;
+  __shared__ unsigned char lab[(kBoxTH + 2 * kR) * kW2];  // halo labels
+  __shared__ unsigned char vlab[kBoxTH * kW2];   // uniform y window: its label
+  __shared__ __attribute__((aligned(16))) unsigned char plab[kBoxTH * kSmTW];  // uniform box: its label
+  __shared__ unsigned short ylist[kBoxTH * kW2];  // mixed y windows
+  __shared__ unsigned short xlist[kBoxTH * kSmTW];  // mixed (boundary) pixels
+  __shared__ int n_list[2];
+  __shared__ vacc_t tbl[2][65];     // raw table entries, widened
+  __shared__ vyf_t yu[2][65];       // y pass of a uniform window, per entry
+  __shared__ tess_v4f xu[2][65];    // final value of a uniform box, per entry
+  __shared__ vyf_t ybuf[kBoxTH * kW2];    // y pass of the mixed windows
+  __shared__ tess_v4f xout[kBoxTH * kSmTW];  // final value of the mixed pixels
+  __shared__ double w[2 * kR + 1];
+  const int DT = D + 1;
+  const int tiles_x = (nx + kSmTW - 1) / kSmTW;
+  const int tid = threadIdx.x, l = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool scrub = flags & SF_EVAL_NAN_SCRUB;
+  const bool be = flags & SF_EVAL_BIG_ENDIAN;
+  const int64_t P = (int64_t)nx * ny;
+  const bool vec = (nx % 4 == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
+  for (int e = tid; e < 2 * R + 1; e += blockDim.x) w[e] = gw[e];
+  // per-entry tables of slot s into buffer b: the raw entry, its uniform y
+  // value and its uniform-box final value (scipy's order on equal inputs)
+  auto entry_tables = [&](int64_t s, int b) {
+    for (int e = tid; e < DT; e += blockDim.x) {
+      const vacc_t t = widen(tab[s * DT + e]);
+      tbl[b][e] = t;
+      vacc_t acc = t * w[R];
+      for (int j = R; j >= 1; --j) acc += (t + t) * w[R - j];
+      vyf_t y;
+#pragma unroll
+      for (int p = 0; p < NP; ++p) y[p] = (float)acc[p];
+      yu[b][e] = y;
+      const vacc_t yd = widen(y);
+      acc = yd * w[R];
+      for (int j = R; j >= 1; --j) acc += (yd + yd) * w[R - j];
+      tess_v4f v;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        float x = (float)acc[p % NP];
+        if (scrub && isnan(x)) x = (p & 1) ? 0.0f : 1.0f;
+        if (be) x = __uint_as_float(__builtin_bswap32(__float_as_uint(x)));
+        v[p] = x;
+      }
+      xu[b][e] = v;
+    }
+  };
+  for (int64_t bb = blockIdx.x; bb < n_tiles * n_sc; bb += gridDim.x) {
+    const int64_t tile = bb % n_tiles, sc = bb / n_tiles;
+    const int tx0 = (int)(tile % tiles_x) * kSmTW;
+    const int ty0 = (int)(tile / tiles_x) * kBoxTH;
+    const int64_t s0 = sc * kBoxSlots;
+    const int ns = (int)((S - s0) < kBoxSlots ? (S - s0) : kBoxSlots);
+    __syncthreads();  // the previous item is done with every LDS array
+    // ---- tile setup, once for the item's slots
+    for (int e = tid; e < H2 * W2; e += blockDim.x) {
+      const int hy = e / W2, hx = e - hy * W2;
+      const int gy = reflect_idx(ty0 + hy - R, ny);
+      const int gx = reflect_idx(tx0 + hx - R, nx);
+      const int lb = labels[(int64_t)gy * nx + gx] - 1;
+      lab[e] = (unsigned char)((lb >= 0 && lb < D) ? lb : D);
+    }
+    if (tid < 2) n_list[tid] = 0;
+    entry_tables(s0, 0);
+    __syncthreads();
+    for (int e = tid; e < kBoxTH * W2; e += blockDim.x) {
+      const int r = e / W2, c = e - r * W2;
+      const unsigned char L = lab[r * W2 + c];
+      bool uni = true;
+      for (int h = 1; h <= 2 * R; ++h) uni &= lab[(r + h) * W2 + c] == L;
+      vlab[e] = uni ? L : kMixed;
+      if (!uni) ylist[atomicAdd(&n_list[0], 1)] = (unsigned short)e;
+    }
+    __syncthreads();
+    for (int e = tid; e < kBoxTH * kSmTW; e += blockDim.x) {
+      const int r = e / kSmTW, x = e - r * kSmTW;
+      const unsigned char* v = vlab + r * W2 + x;
+      const unsigned char L = v[0];
+      bool uni = L != kMixed;
+      for (int j = 1; j <= 2 * R; ++j) uni &= v[j] == L;
+      plab[e] = uni ? L : kMixed;
+      if (!uni && ty0 + r < ny && tx0 + x < nx)
+        xlist[atomicAdd(&n_list[1], 1)] = (unsigned short)e;
+    }
+    __syncthreads();
+    const int ny_list = n_list[0], nx_list = n_list[1];
+    for (int k = 0; k < ns; ++k) {
+      const int b = k & 1;
+      const vacc_t* t = tbl[b];
+      // y pass of the mixed windows (fp64 in scipy's order, float result)
+      for (int i = tid; i < ny_list; i += blockDim.x) {
+        const int e = ylist[i];
+        const int r = e / W2, c = e - r * W2;
+        const unsigned char* col = lab + (r + R) * W2 + c;
+        vacc_t acc = t[col[0]] * w[R];
+#pragma unroll kTapUnroll
+        for (int j = R; j >= 1; --j) acc += (t[col[-j * W2]] + t[col[j * W2]]) * w[R - j];
+        vyf_t y;
+#pragma unroll
+        for (int p = 0; p < NP; ++p) y[p] = (float)acc[p];
+        ybuf[e] = y;
+      }
+      __syncthreads();
+      // x pass of the mixed pixels: a window's y value from ybuf (mixed) or
+      // from the per-entry table (uniform)
+      for (int i = tid; i < nx_list; i += blockDim.x) {
+        const int e = xlist[i];
+        const int r = e / kSmTW, x = e - r * kSmTW;
+        const int c0 = r * W2 + x + R;
+        auto ycol = [&](int c) -> vacc_t {
+          const unsigned char L = vlab[c];
+          return widen(L != kMixed ? yu[b][L] : ybuf[c]);
+        };
+        vacc_t acc = ycol(c0) * w[R];
+#pragma unroll kTapUnroll
+        for (int j = R; j >= 1; --j) acc += (ycol(c0 - j) + ycol(c0 + j)) * w[R - j];
+        tess_v4f v;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          float xv = (float)acc[p % NP];
+          if (scrub && isnan(xv)) xv = (p & 1) ? 0.0f : 1.0f;
+          if (be) xv = __uint_as_float(__builtin_bswap32(__float_as_uint(xv)));
+          v[p] = xv;
+        }
+        xout[e] = v;
+      }
+      __syncthreads();
+      // stores: wave w writes tile row w, 4 pixels per lane (1 KiB runs per
+      // plane); then the next slot's per-entry tables into the other buffer
+      {
+        const int gy = ty0 + wv, gx0 = tx0 + 4 * l;
+        if (gy < ny && gx0 < nx) {
+          const int e0 = wv * kSmTW + 4 * l;
+          const unsigned pl = *reinterpret_cast<const unsigned*>(plab + e0);
+          tess_v4f v[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const unsigned L = (pl >> (8 * i)) & 0xFF;
+            v[i] = L != kMixed ? xu[b][L] : xout[e0 + i];
+          }
+          const int64_t so = (s0 + k + ring_base) % ring;
+          float* o = out + so * 4 * P + (int64_t)gy * nx + gx0;
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            if (vec) {
+              __builtin_nontemporal_store(tess_v4f{v[0][p], v[1][p], v[2][p], v[3][p]},
+                                          reinterpret_cast<tess_v4f*>(o + p * P));
+            } else {
+#pragma unroll
+              for (int i = 0; i < 4; ++i)
+                if (gx0 + i < nx) o[p * P + i] = v[i][p];
+            }
+          }
+        }
+      }
+      if (k + 1 < ns) entry_tables(s0 + k + 1, b ^ 1);
+      __syncthreads();
+    }
+  }
+}
+
 // Separable Gaussian of Screen.write for any radius (screen.py:353-362:
 // scipy.ndimage.gaussian_filter(img, sigma=(0, s, s)) per (time, freq,
 // station), i.e. per image of the [.][4][ny][nx] cube): one 1-D pass per
@@ -530,7 +738,14 @@ int launch_tess(sf_ctx* ctx, const int32_t* labels, int nx, int ny,
                 int64_t ring, const double* d_w, int R, unsigned flags) {
   const int64_t P = (int64_t)nx * ny;
   const int64_t DT = D + 1;
-  int chunk = kSmSlots;
+  // smoothing: the interior-lookup kernel or the wide-tile kernel
+  // (SF_OPT_TESS_BOX; auto: interior lookups for four planes at R <= 2, where
+  // the wide-tile kernel is fp64-VALU-bound -- sigma 0.5 px, 26 -> 18 ms per
+  // 102,400 256^2 slots; with two planes, or wider, its sliding windows win:
+  // profiles/round3o_tess_box_ab.txt)
+  const bool box = R > 0 && R <= kBoxMaxR &&
+                   (ctx->tess_box == 1 || (ctx->tess_box < 0 && amp_yy && R <= 2));
+  int chunk = box ? kBoxSlots : kSmSlots;
   if (R == 0) {
     // the item's table slice in LDS: at most 64 KiB (63 slots at D = 64)
     chunk = ctx->tess_slots > 0 ? ctx->tess_slots : kGatherSlotsAuto;
@@ -551,6 +766,39 @@ int launch_tess(sf_ctx* ctx, const int32_t* labels, int nx, int ny,
                        amp_yy ? amp_yy + b * D : nullptr, D, Sb, tab, tab_flags);
     SF_HIP(hipGetLastError());
     const int64_t n_sc = (Sb + chunk - 1) / chunk;
+    if (box) {
+      const int64_t n_tiles = (int64_t)((nx + kSmTW - 1) / kSmTW) * ((ny + kBoxTH - 1) / kBoxTH);
+      int64_t grid = n_tiles * n_sc;
+      const int64_t cap = ((int64_t)1 << 31) / 256;
+      if (grid > cap) grid = cap;  // workgroups walk the remaining items
+#define SF_BOX(RT)                                                                  \
+  do {                                                                              \
+    if (amp_yy)                                                                     \
+      hipLaunchKernelGGL((kl_tess_box_kernel<RT, 4>), dim3((unsigned)grid),         \
+                         dim3(256), 0, ctx->stream, labels, nx, ny, tab, D, Sb, out, \
+                         ring, b % ring, d_w, R, n_tiles, n_sc, flags);             \
+    else                                                                            \
+      hipLaunchKernelGGL((kl_tess_box_kernel<RT, 2>), dim3((unsigned)grid),         \
+                         dim3(256), 0, ctx->stream, labels, nx, ny, tab, D, Sb, out, \
+                         ring, b % ring, d_w, R, n_tiles, n_sc, flags);             \
+  } while (0)
+      // compiled radii: sigma up to 2 px (R <= 8); wider ones run the
+      // run-time radius variant
+      switch (R) {
+        case 1: SF_BOX(1); break;
+        case 2: SF_BOX(2); break;
+        case 3: SF_BOX(3); break;
+        case 4: SF_BOX(4); break;
+        case 5: SF_BOX(5); break;
+        case 6: SF_BOX(6); break;
+        case 7: SF_BOX(7); break;
+        case 8: SF_BOX(8); break;
+        default: SF_BOX(0);
+      }
+#undef SF_BOX
+      SF_HIP(hipGetLastError());
+      continue;
+    }
     if (R > 0) {
       const int rows = smooth_rows(R);  // the kernel's kSmTH (8 for every R > 2)
       const int64_t n_tiles = (int64_t)((nx + kSmTW - 1) / kSmTW) * ((ny + rows - 1) / rows);

@@ -381,16 +381,18 @@ def test_tess_gather_amplitudes_nan_byteswap(n, S):
                                          (96, 40, 2.5), (40, 96, 5.0),
                                          (300, 260, 4.0), (64, 64, 6.0), (20, 9, 0.3)])
 def test_tess_kernels_agree_with_tile_kernel(nx, ny, sigma):
-    """The table + gather (R = 0) and wide-tile smoothing (R <= 24) kernels
-    write the same bits as the round-1 fused 16 x 16 tile kernel
-    (SF_OPT_TESS_TILE): ragged tiles and slot chunks, NaN phases and
-    amplitudes, labels of every cell, scrub / byte-swap flags."""
+    """The table + gather (R = 0), interior-lookup smoothing (R <= 24,
+    SF_OPT_TESS_BOX = 1) and wide-tile smoothing kernels write the
+    same bits as the round-1 fused 16 x 16 tile kernel (SF_OPT_TESS_TILE):
+    ragged tiles and slot chunks, NaN phases and amplitudes, labels of every
+    cell (noise, so most pixels are cell boundaries) next to a constant
+    region (interior pixels), scrub / byte-swap flags."""
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from ska_sdp_screen_fitting_amd import get_context
     from ska_sdp_screen_fitting_amd._lib import (SF_EVAL_BIG_ENDIAN, SF_EVAL_NAN_SCRUB,
-                                                 SF_OPT_TESS_TILE)
+                                                 SF_OPT_TESS_BOX, SF_OPT_TESS_TILE)
     dev = torch.device("cuda", 0)
     ctx = get_context(0)
     ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
@@ -409,15 +411,64 @@ def test_tess_kernels_agree_with_tile_kernel(nx, ny, sigma):
     for flags, yy in ((SF_EVAL_NAN_SCRUB, None), (SF_EVAL_NAN_SCRUB | SF_EVAL_BIG_ENDIAN, None),
                       (0, None), (SF_EVAL_NAN_SCRUB, t["ay"]), (0, t["ay"])):
         res = []
-        for tile in (0, 1):
+        for tile, box in ((1, 1), (0, 1), (0, 0)):
             out = torch.full((S, 4, ny, nx), -5.0, dtype=torch.float32, device=dev)
             ctx.set_option(SF_OPT_TESS_TILE, tile)
+            ctx.set_option(SF_OPT_TESS_BOX, box)
             try:
                 ctx.tess_fill(t["lab"], nx, ny, t["ph"], D, S, out, amp_xx=t["ax"],
                               amp_yy=yy, smooth_pix=sigma, flags=flags)
                 torch.cuda.synchronize()
             finally:
                 ctx.set_option(SF_OPT_TESS_TILE, 0)
+                ctx.set_option(SF_OPT_TESS_BOX, -1)
             res.append(out.cpu().numpy().view(np.uint32))
-        assert np.array_equal(res[0], res[1]), (flags, yy is None,
-                                                int((res[0] != res[1]).sum()))
+        for k in (1, 2):
+            assert np.array_equal(res[0], res[k]), (k, flags, yy is None,
+                                                    int((res[0] != res[k]).sum()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cell,sigma,gain", [(0.02602, 0.5, False), (0.02602, 0.5, True),
+                                             (0.01301, 0.5, True), (0.01301, 2.0, False),
+                                             (0.01301, 3.0, True), (0.05, 6.0, False)])
+def test_tess_box_kernel_on_voronoi_rasters(cell, sigma, gain):
+    """The interior-lookup smoothing kernel on the fixture's own Voronoi
+    rasters (large uniform cells: most pixels take the per-cell value)
+    writes the same bits as the wide-tile kernel that sums every pixel, and
+    matches scipy within 1e-6 (x max(1, A))."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from ska_sdp_screen_fitting_amd import get_context
+    from ska_sdp_screen_fitting_amd._lib import SF_EVAL_NAN_SCRUB, SF_OPT_TESS_BOX
+    dev = torch.device("cuda", 0)
+    ctx = get_context(0)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    g, radec = fixture_patches()
+    lab, _ = tessellation_template(radec, FIELD["rad"], FIELD["dec"], FIELD["width"], cell)
+    ny, nx = lab.shape
+    ref = int(g["ref_ant"])
+    ph = (g["val"] - g["val"][:, :, ref:ref + 1, :])[:, 5].reshape(-1, 7)[:40]
+    ph[3, 2] = np.nan
+    S, D = ph.shape
+    rng = np.random.default_rng(3)
+    ax = 10.0 ** rng.normal(0.0, 0.1, size=(S, D)) if gain else None
+    ay = 10.0 ** rng.normal(0.0, 0.1, size=(S, D)) if gain else None
+    dv = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    lab_d = torch.from_numpy(np.ascontiguousarray(lab, np.int32)).to(dev)
+    res = []
+    for box in (1, 0):
+        out = torch.full((S, 4, ny, nx), -5.0, dtype=torch.float32, device=dev)
+        ctx.set_option(SF_OPT_TESS_BOX, box)
+        try:
+            ctx.tess_fill(lab_d, nx, ny, dv(ph), D, S, out, amp_xx=dv(ax), amp_yy=dv(ay),
+                          smooth_pix=sigma, flags=SF_EVAL_NAN_SCRUB)
+            torch.cuda.synchronize()
+        finally:
+            ctx.set_option(SF_OPT_TESS_BOX, -1)
+        res.append(out.cpu().numpy())
+    assert np.array_equal(res[0].view(np.uint32), res[1].view(np.uint32))
+    want = _scrub(ov.smooth(ov.gather_planes(lab, ph, ax, ay), sigma))
+    scale = np.maximum(1.0, np.abs(want))
+    assert np.max(np.abs(res[0] - want) / scale) <= 1e-6
