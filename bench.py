@@ -650,7 +650,7 @@ def tess_steps(args, ctx, torch, dev, dist, world, rank, coll_dev, sol, setup,
         # the library's choice (tess.hip launch_tess, SF_OPT_TESS_BOX auto)
         R = int(4.0 * args.smooth_pix + 0.5) if args.smooth_pix > 0 else 0
         box = 0 < R <= 24 and (args.tess_box == 1 or (args.tess_box < 0 and
-                                                       args.tess_gain and R <= 2))
+                                                       args.tess_gain and R <= 5))
         kernel = ("kl_tess_gather_kernel" if R == 0 else
                   "kl_tess_box_kernel" if box else "kl_tess_smooth_kernel")
         # PMC traffic (profiles/traffic.json) when measured on this call shape

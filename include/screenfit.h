@@ -164,7 +164,7 @@ int sf_device_cus(sf_ctx* ctx, int* n_cu);
  * the pixels whose whole (2R + 1)^2 neighbourhood is one cell from a
  * per-(slot, cell) value and sums only the others (kl_tess_box_kernel); 0:
  * the wide-tile kernel that sums every pixel; -1 (default): the first for
- * four planes (XX / YY amplitudes) at radius <= 2, else the second.  Same
+ * four planes (XX / YY amplitudes) at radius <= 5, else the second.  Same
  * bits. */
 #define SF_OPT_TESS_BOX 14
 #define SF_EVAL_KERNEL_AUTO 0

@@ -739,12 +739,13 @@ int launch_tess(sf_ctx* ctx, const int32_t* labels, int nx, int ny,
   const int64_t P = (int64_t)nx * ny;
   const int64_t DT = D + 1;
   // smoothing: the interior-lookup kernel or the wide-tile kernel
-  // (SF_OPT_TESS_BOX; auto: interior lookups for four planes at R <= 2, where
-  // the wide-tile kernel is fp64-VALU-bound -- sigma 0.5 px, 26 -> 18 ms per
-  // 102,400 256^2 slots; with two planes, or wider, its sliding windows win:
-  // profiles/round3o_tess_box_ab.txt)
+  // (SF_OPT_TESS_BOX; auto: interior lookups for four planes at R <= 5, where
+  // the wide-tile kernel is fp64-VALU-bound -- sigma 0.25 / 0.5 / 0.75 / 1 /
+  // 1.25 px: 0.66 / 0.51 / 0.42 / 0.35 / 0.31 -> 0.73 / 0.73 / 0.59 / 0.44 /
+  // 0.37 of 8 TB/s; with two planes, or at R = 8, the wide-tile kernel's
+  // sliding windows win: profiles/round3p_tess_box_sweep.txt)
   const bool box = R > 0 && R <= kBoxMaxR &&
-                   (ctx->tess_box == 1 || (ctx->tess_box < 0 && amp_yy && R <= 2));
+                   (ctx->tess_box == 1 || (ctx->tess_box < 0 && amp_yy && R <= 5));
   int chunk = box ? kBoxSlots : kSmSlots;
   if (R == 0) {
     // the item's table slice in LDS: at most 64 KiB (63 slots at D = 64)
