@@ -96,6 +96,9 @@ def parse():
     ap.add_argument("--eval-xcd-map", type=int, default=-1,
                     help="SF_OPT_EVAL_XCD_MAP: -1 auto (default), 0 contiguous "
                          "pixel blocks per XCD, 1 interleaved")
+    ap.add_argument("--eval-int", type=int, default=-1, choices=(-1, 0),
+                    help="SF_OPT_EVAL_INT: -1 the integer-digit contraction where "
+                         "it applies (phase D >= 45, gain screens), 0 fp64 MFMAs")
     ap.add_argument("--eval-groups", type=int, default=0,
                     help="SF_OPT_EVAL_GROUPS: most 16-slot groups per eval work "
                          "item (0 = library default)")
@@ -731,6 +734,7 @@ def main():
                                                  SF_EVAL_NAN_SCRUB,
                                                  SF_EVAL_NT_STORES,
                                                  SF_OPT_EVAL_GROUPS,
+                                                 SF_OPT_EVAL_INT,
                                                  SF_OPT_EVAL_XCD_MAP)
     from ska_sdp_screen_fitting_amd.distributed import setup_shard
     from ska_sdp_screen_fitting_amd._lib import SF_SCREEN_AMPLITUDE
@@ -841,6 +845,7 @@ def main():
 
     ctx.set_option(SF_OPT_EVAL_XCD_MAP, args.eval_xcd_map)
     ctx.set_option(SF_OPT_EVAL_GROUPS, args.eval_groups)
+    ctx.set_option(SF_OPT_EVAL_INT, args.eval_int)
     eval_kernel_name = ctx.eval_kernel(flags, gain=gain)
     # discard + checksum mode: the cubes go
     # through the HBM ring and every slot's checksum is accumulated

@@ -167,6 +167,17 @@ int sf_device_cus(sf_ctx* ctx, int* n_cu);
  * four planes (XX / YY amplitudes) at radius <= 5, else the second.  Same
  * bits. */
 #define SF_OPT_TESS_BOX 14
+/* SF_OPT_EVAL_INT = 0 evaluates with the fp64 MFMA contraction everywhere;
+ * -1 (default): the integer-digit contraction -- Cpix and the coefficients
+ * as 6 balanced base-256 digits of 36- / 44-bit fixed point, contracted
+ * exactly on i8 MFMAs (64x the fp64 MFMA rate per product) modulo 2^32
+ * turns -- for phase screens with D >= 45 and for gain screens, on the fast
+ * (hardware sincos) epilogue with float4-aligned output; slots whose
+ * coefficients are not finite or out of the digit range take the fp64
+ * contraction.  |error| <= 2^-28 turn of phase (2^-32 typical), below the
+ * fp32 rounding of the reduced phase; while it applies every kernel request
+ * runs the register tile (sf_get_eval_kernel says so). */
+#define SF_OPT_EVAL_INT 15
 #define SF_EVAL_KERNEL_AUTO 0
 #define SF_EVAL_KERNEL_TILE 1
 #define SF_EVAL_KERNEL_LDS4 2

@@ -91,6 +91,9 @@ int sf_destroy(sf_ctx* ctx) {
   hipFree(ctx->d_u);
   hipFree(ctx->d_eig);
   hipFree(ctx->d_cfrag);
+  hipFree(ctx->d_cdig);
+  hipFree(ctx->d_kdig);
+  hipFree(ctx->d_kflag);
   hipFree(ctx->d_skip);
   hipFree(ctx->d_st_order);
   hipFree(ctx->d_keys);
@@ -221,6 +224,11 @@ int sf_set_option(sf_ctx* ctx, int option, int value) {
     case SF_OPT_EVAL_MAX_BLOCKS:
       SF_REQUIRE(value >= 0, SF_EINVAL, "sf_set_option: negative block cap");
       ctx->eval_max_blocks = value;
+      return SF_OK;
+    case SF_OPT_EVAL_INT:
+      SF_REQUIRE(value == -1 || value == 0, SF_EINVAL,
+                 "sf_set_option: eval int must be -1 or 0");
+      ctx->eval_int = value;
       return SF_OK;
     default:
       set_error("sf_set_option: unknown option");
@@ -417,6 +425,29 @@ int sf_set_grid(sf_ctx* ctx, const double* x, int nx, const double* y,
   } else {
     rc = sf::launch_cpix(ctx, dx, dy);
   }
+  // largest |Cpix| over the grid (kl_cpix_kernel's formula on the farthest
+  // corner of each direction, 1 % margin for the device pow): the
+  // fixed-point phase epilogue's group bound and the integer contraction's
+  // range check
+  double cmax = 0.0;
+  for (int d = 0; d < ctx->D; ++d) {
+    double mx = 0.0, my = 0.0;
+    for (int i = 0; i < nx; ++i) mx = std::fmax(mx, std::fabs(ctx->h_pp[3 * d] - x[i]));
+    for (int j = 0; j < ny; ++j) my = std::fmax(my, std::fabs(ctx->h_pp[3 * d + 1] - y[j]));
+    const double z = ctx->h_pp[3 * d + 2];
+    const double d2 = mx * mx + my * my + z * z;
+    cmax = std::fmax(cmax, 1.01 * 0.5 * std::pow(d2 / (ctx->r0 * ctx->r0), ctx->beta / 2.0));
+  }
+  // the integer-digit contraction (D >= 45): rint(Cpix * 2^36) must fit 6
+  // balanced base-256 digits (|.| < 2^46.99); 2^46.9 leaves the margin
+  ctx->dig_ok = 0;
+  if (rc == SF_OK && ctx->ksteps >= 12 && std::isfinite(cmax) &&
+      cmax * 68719476736.0 < std::ldexp(1.0, 46) * 1.86) {
+    rc = dev_alloc(&ctx->d_cdig, (size_t)ctx->n_pix_blocks * sf::kEvalWaves *
+                                     sf::kDigits * sf::kTiles * 64 * 16);
+    if (rc == SF_OK) rc = sf::launch_cdig(ctx, dx, dy);
+    if (rc == SF_OK) ctx->dig_ok = 1;
+  }
   if (hipStreamSynchronize(ctx->stream) != hipSuccess && rc == SF_OK) {
     set_error("sf_set_grid: pixel basis kernel failed");
     rc = SF_EIO;
@@ -424,22 +455,11 @@ int sf_set_grid(sf_ctx* ctx, const double* x, int nx, const double* y,
   (void)hipFree(dx);
   (void)hipFree(dy);
   if (rc == SF_OK) {
-    // largest |Cpix| over the grid (kl_cpix_kernel's formula on the farthest
-    // corner of each direction, 1 % margin for the device pow): the
-    // fixed-point phase epilogue's group bound
-    double cmax = 0.0;
-    for (int d = 0; d < ctx->D; ++d) {
-      double mx = 0.0, my = 0.0;
-      for (int i = 0; i < nx; ++i) mx = std::fmax(mx, std::fabs(ctx->h_pp[3 * d] - x[i]));
-      for (int j = 0; j < ny; ++j) my = std::fmax(my, std::fabs(ctx->h_pp[3 * d + 1] - y[j]));
-      const double z = ctx->h_pp[3 * d + 2];
-      const double d2 = mx * mx + my * my + z * z;
-      cmax = std::fmax(cmax, 0.5 * std::pow(d2 / (ctx->r0 * ctx->r0), ctx->beta / 2.0));
-    }
-    cmax *= 1.01;
     // per lane (a quarter of a slot's directions): 2^17 / 4 turns
     ctx->rev_thr = cmax > 0.0 && std::isfinite(cmax) ? 32768.0 / cmax : 0.0;
     ctx->n_pix = n_pix;
+  } else {
+    ctx->dig_ok = 0;
   }
   return rc;
 }

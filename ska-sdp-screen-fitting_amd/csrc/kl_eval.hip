@@ -84,6 +84,55 @@ int launch_cpix(sf_ctx* ctx, const double* d_x, const double* d_y) {
   return SF_OK;
 }
 
+// Pixel digits of the integer contraction (kl_eval_int.h): digit i of a
+// wave pixel block in v_mfma_i32_16x16x64_i8 B order -- lane l, byte jb holds
+// direction d = 16 (l >> 4) + jb of pixel column l & 15 of tile t, i.e. digit
+// i of rint(Cpix[p][d] * 2^36) (0 past D or the grid).  Cpix is
+// kl_cpix_kernel's value bit for bit (pix_cov).
+__global__ __launch_bounds__(256) void kl_cdig_kernel(
+    const double* __restrict__ pp, int D, double r0, double beta,
+    const double* __restrict__ xs, int nx, const double* __restrict__ ys,
+    int ny, int64_t n_frag, v4i* __restrict__ cdig) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n_frag) return;
+  const int l = (int)(e & 63);
+  const int t = (int)((e >> 6) % kTiles);
+  const int64_t rest = (e >> 6) / kTiles;
+  const int i = (int)(rest % kDigits);
+  const int64_t wpb = rest / kDigits;
+  const int64_t p = wpb * kWavePix + (int64_t)(l & 15) * kTiles + t;
+  union {
+    v4i v;
+    int8_t b[16];
+  } u;
+#pragma unroll 1
+  for (int jb = 0; jb < 16; ++jb) {
+    const int d = 16 * (l >> 4) + jb;
+    int8_t val = 0;
+    if (d < D && p < (int64_t)nx * ny) {
+      const int ix = (int)(p % nx), iy = (int)(p / nx);
+      const double c = pix_cov(pp[3 * d], pp[3 * d + 1], pp[3 * d + 2], xs[ix], ys[iy],
+                               r0 * r0, beta / 2.0);
+      int8_t dg[kDigits];
+      (void)dig_split((long long)rint(ldexp(c, kSigma)), dg);  // fits: sf_set_grid
+      val = dg[i];
+    }
+    u.b[jb] = val;
+  }
+  cdig[e] = u.v;
+}
+
+int launch_cdig(sf_ctx* ctx, const double* d_x, const double* d_y) {
+  const int64_t n_wpb = ctx->n_pix_blocks * kEvalWaves;
+  const int64_t n = n_wpb * kDigits * kTiles * 64;
+  const int64_t blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(kl_cdig_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                     ctx->stream, ctx->d_pp, ctx->D, ctx->r0, ctx->beta, d_x,
+                     ctx->nx, d_y, ctx->ny, n, reinterpret_cast<v4i*>(ctx->d_cdig));
+  SF_HIP(hipGetLastError());
+  return SF_OK;
+}
+
 // Kernel sf_kl_eval runs for this context, output alignment and flags.
 int pick_eval_kernel(const sf_ctx* ctx, bool gain, unsigned flags,
                      bool out_aligned16) {
@@ -93,6 +142,14 @@ int pick_eval_kernel(const sf_ctx* ctx, bool gain, unsigned flags,
   const bool lds_ok = !gain && (flags & SF_EVAL_FAST_SINCOS) &&
                       (ctx->n_pix % 4 == 0) && out_aligned16;
   const int opt = ctx->eval_kernel;
+  // the integer-digit contraction (phase D >= 45) runs on the register tile
+  // and the LDS-staged kernels (same bits); SHB keeps fp64 fragments in LDS
+  // and is replaced by the register tile there
+  const bool ic = eval_int_applies(ctx, gain, flags, out_aligned16);
+  if (ic && opt == SF_EVAL_KERNEL_SHB) return SF_EVAL_KERNEL_TILE;
+  // (auto: the register tile -- 512^2 x D = 50 0.744 with 4-group items;
+  // the LDS-staged shapes 0.66-0.70, profiles/round3y_eval_items_512.txt)
+  if (ic && opt == SF_EVAL_KERNEL_AUTO) return SF_EVAL_KERNEL_TILE;
   if (opt == SF_EVAL_KERNEL_SHB)
     return (!gain && ctx->n_pix % 4 == 0 && out_aligned16) ? opt : SF_EVAL_KERNEL_TILE;
   if (opt == SF_EVAL_KERNEL_TILE || opt == SF_EVAL_KERNEL_TILE3) return opt;

@@ -9,6 +9,7 @@
 #include <cmath>
 #include <type_traits>
 
+#include "kl_eval_int.h"
 #include "sf_internal.h"
 
 namespace sf {
@@ -363,16 +364,21 @@ __device__ __forceinline__ float amp2f(double log2a) {
 // a 64-bit product and the trash select (a run-time choice between the two
 // would again be a branch round the stores, see BEM)
 template <int KS, int MINW, bool VEC4, bool FAST, bool NT, bool GAIN,
-          bool SHB = false, int BEM = 2, bool DIRECT = false>
+          bool SHB = false, int BEM = 2, bool DIRECT = false, bool IC = false>
 __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
     const double* __restrict__ cfrag, const double* __restrict__ coef,
     const double* __restrict__ coef_xx, const double* __restrict__ coef_yy,
     int D, int64_t S, int64_t P, int64_t n_pb, int64_t n_sc, int chunk_groups,
     float* __restrict__ out, int64_t ring, int64_t ring_base, unsigned flags,
-    unsigned* __restrict__ sums, float* __restrict__ trash, double rev_thr) {
+    unsigned* __restrict__ sums, float* __restrict__ trash, double rev_thr,
+    DigArgs dg) {
   constexpr int kFrag = KS * kTiles * 64;  // Cpix doubles of a wave pixel block
+  // IC: the integer-digit contraction (kl_eval_int.h) instead of the fp64
+  // MFMAs; slots it cannot carry take the fp64 contraction with the Cpix
+  // fragments read from memory
+  static_assert(!IC || (FAST && !SHB && !GAIN), "integer contraction: fast phase register tile");
   // fixed-point phase reduction (kRevMagic) for D <= 44
-  constexpr bool kMagic = FAST && KS <= kMagicMaxKS;
+  constexpr bool kMagic = FAST && KS <= kMagicMaxKS && !IC;
   __shared__ double bsh[SHB ? kFrag : 1];
   const int l = threadIdx.x & 63;
   // wave index, wave-uniform: keeps slot / ring arithmetic on the SALU
@@ -394,13 +400,22 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
     }
     if (wpb * kWavePix >= P) continue;
 
-    double bf[SHB ? 1 : KS][kTiles];
-    if constexpr (!SHB) {
+    double bf[SHB || IC ? 1 : KS][kTiles];
+    if constexpr (!SHB && !IC) {
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
         for (int t = 0; t < kTiles; ++t)
           bf[kk][t] = cfrag[((wpb * KS + kk) * kTiles + t) * 64 + l];
+    }
+    // IC: the pixel digit fragments [tile][digit]
+    v4i bd[kTiles][IC ? kDigits : 1];
+    if constexpr (IC) {
+#pragma unroll
+      for (int t = 0; t < kTiles; ++t)
+#pragma unroll
+        for (int i = 0; i < kDigits; ++i)
+          bd[t][i] = dg.cdig[((wpb * kDigits + i) * kTiles + t) * 64 + l];
     }
     auto bval = [&](int kk, int t) -> double {
       if constexpr (SHB) return bsh[(kk * kTiles + t) * 64 + l];
@@ -435,7 +450,32 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
     double rf[KS], rx[GAIN ? KS : 1], ry[GAIN ? KS : 1];
     double af[KS], ax[GAIN ? KS : 1], ay[GAIN ? KS : 1];
     bool safe = false;
-    {
+    // IC: the digit rows and the slot flags, one group ahead (the A-lane
+    // feeding group row m holds slot dig_row_slot); unconditional loads of a
+    // clamped slot (a load behind a branch is a serial round trip), slots
+    // past S count as carried
+    const int rs = dig_row_slot(l);
+    DigRows wp;
+    bool okp = true;
+    auto load_flag = [&](int64_t s) {
+      const uint8_t f = dg.kflag[s < S ? s : S - 1];
+      okp = s >= S || f != 0;
+    };
+    if constexpr (IC) {
+      dig_load(wp, dg.kdig, slot_base + rs, S, l);
+      load_flag(slot_base + rs);
+      // everything loaded so far must have landed before the group loop (as
+      // the Cpix fragments below): else the compiler, merging this path with
+      // the loop's back edge, waits at the loop top with a count that covers
+      // the previous group's stores as well
+#pragma unroll
+      for (int t = 0; t < kTiles; ++t)
+#pragma unroll
+        for (int i = 0; i < kDigits; ++i) asm volatile("" ::"v"(bd[t][i]));
+#pragma unroll
+      for (int n = 0; n < kDigits; ++n) asm volatile("" ::"v"(wp.w[n]));
+      asm volatile("" ::"s"(__builtin_amdgcn_ballot_w64(okp)));
+    } else {
       const int64_t s0 = slot_base + (SHB ? w : 0) * 16;
       load_coef_raw<KS>(rf, coef, s0, S, D, l);
       coef_finish<KS>(af, rf, s0, S, D, l, kInv2Pi);  // phase in turns
@@ -465,10 +505,12 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
       if constexpr (SHB) asm volatile("" ::: "memory");
       // the next group's loads (a clamped dummy past the chunk or S)
       const int64_t s1 = s0 + 16 * kGStep;
-      load_coef_raw<KS>(rf, coef, s1, S, D, l);
-      if constexpr (GAIN) {
-        load_coef_raw<KS>(rx, coef_xx, s1, S, D, l);
-        load_coef_raw<KS>(ry, coef_yy, s1, S, D, l);
+      if constexpr (!IC) {
+        load_coef_raw<KS>(rf, coef, s1, S, D, l);
+        if constexpr (GAIN) {
+          load_coef_raw<KS>(rx, coef_xx, s1, S, D, l);
+          load_coef_raw<KS>(ry, coef_yy, s1, S, D, l);
+        }
       }
       // ring slot of the group's first slot (S, ring < 2^31: launch_eval);
       // the 16 rows follow it with at most one wrap when the ring is >= 16
@@ -477,48 +519,97 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
       // fast epilogue: fixed-point phase accumulators (kRevMagic)
       const double a0 = kMagic ? kRevMagic : 0.0;
       v4d acc[kTiles];
-#pragma unroll
-      for (int t = 0; t < kTiles; ++t) acc[t] = v4d{a0, a0, a0, a0};
-#pragma unroll
-      for (int kk = 0; kk < KS; ++kk)
-#pragma unroll
-        for (int t = 0; t < kTiles; ++t)
-          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[kk], bval(kk, t),
-                                                        acc[t], 0, 0, 0);
       // gain: the XX / YY log-amplitude screens share the pixel basis
       v4d accx[GAIN ? kTiles : 1], accy[GAIN ? kTiles : 1];
-      if constexpr (GAIN) {
+      // fast epilogue: the reduced phases of the group's 4 x 4 values
+      float frg[4][kTiles];
+      if constexpr (!IC) {
 #pragma unroll
-        for (int t = 0; t < kTiles; ++t) {
-          accx[t] = v4d{0.0, 0.0, 0.0, 0.0};
-          accy[t] = v4d{0.0, 0.0, 0.0, 0.0};
-        }
+        for (int t = 0; t < kTiles; ++t) acc[t] = v4d{a0, a0, a0, a0};
 #pragma unroll
         for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
+          for (int t = 0; t < kTiles; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[kk], bval(kk, t),
+                                                          acc[t], 0, 0, 0);
+        if constexpr (GAIN) {
+#pragma unroll
           for (int t = 0; t < kTiles; ++t) {
-            accx[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ax[kk], bval(kk, t), accx[t], 0, 0, 0);
-            accy[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ay[kk], bval(kk, t), accy[t], 0, 0, 0);
+            accx[t] = v4d{0.0, 0.0, 0.0, 0.0};
+            accy[t] = v4d{0.0, 0.0, 0.0, 0.0};
           }
-      }
-      // fast epilogue: the reduced phases of the group's 4 x 4 values, fixed
-      // point or exact by ONE wave-uniform branch per group (per-row
-      // branches measured 4 % slower at D = 50); gain screens scrub the
-      // products, phase screens the reduced argument (cos 1, sin 0)
-      float frg[4][kTiles];
-      if constexpr (FAST) {
-        if (safe) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
+          for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
-            for (int t = 0; t < kTiles; ++t) frg[r][t] = rev_fixed(acc[t][r]);
-        } else {
+            for (int t = 0; t < kTiles; ++t) {
+              accx[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ax[kk], bval(kk, t), accx[t], 0, 0, 0);
+              accy[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ay[kk], bval(kk, t), accy[t], 0, 0, 0);
+            }
+        }
+        // fixed point or exact by ONE wave-uniform branch per group (per-row
+        // branches measured 4 % slower at D = 50); gain screens scrub the
+        // products, phase screens the reduced argument (cos 1, sin 0)
+        if constexpr (FAST) {
+          if (safe) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+              for (int t = 0; t < kTiles; ++t) frg[r][t] = rev_fixed(acc[t][r]);
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              double rv[kTiles];
+#pragma unroll
+              for (int t = 0; t < kTiles; ++t) rv[t] = acc[t][r] - a0;
+              rev_reduce_n<kTiles>(frg[r], rv, !GAIN && scrub);
+            }
+          }
+        }
+      } else {
+        // ---- integer-digit contraction (kl_eval_int.h)
+        // rows the digits cannot carry (bit 4 (l >> 4) + r <-> lane l's
+        // register r): this group's flags, loaded one group ahead
+        const unsigned long long badp = __builtin_amdgcn_ballot_w64(!okp) & 0xffffull;
+        const int rowbit = 4 * (l >> 4);
+#pragma unroll
+        for (int t = 0; t < kTiles; ++t) {
+          const v4i R = dig_contract(wp, bd[t]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) frg[r][t] = (float)R[r] * kTwoM32;
+        }
+        // the next group's rows and flags (wp is free now)
+        dig_load(wp, dg.kdig, s1 + rs, S, l);
+        load_flag(s1 + rs);
+        // fp64 contraction of the rows the digits cannot carry (non-finite
+        // or out-of-range coefficients; rare), one k-step at a time (few
+        // registers beside the digit fragments), Cpix fragments from memory:
+        // the same products in the same order as the fp64 register tile, the
+        // exact reduction
+        if (badp != 0ull) {
+          const int64_t sa = s0 + (l & 15);
+          const double* row = coef + (sa < S ? sa : S - 1) * D;
+          v4d ac[kTiles];
+#pragma unroll
+          for (int t = 0; t < kTiles; ++t) ac[t] = v4d{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 1
+          for (int kk = 0; kk < KS; ++kk) {
+            const int d = 4 * kk + (l >> 4);
+            const double a = keep_if(sa < S && d < D, row[d < D ? d : D - 1] * kInv2Pi);
+#pragma unroll
+            for (int t = 0; t < kTiles; ++t)
+              ac[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(
+                  a, cfrag[((wpb * KS + kk) * kTiles + t) * 64 + l], ac[t], 0, 0, 0);
+          }
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             double rv[kTiles];
+            float f[kTiles];
 #pragma unroll
-            for (int t = 0; t < kTiles; ++t) rv[t] = acc[t][r] - a0;
-            rev_reduce_n<kTiles>(frg[r], rv, !GAIN && scrub);
+            for (int t = 0; t < kTiles; ++t) rv[t] = ac[t][r];
+            rev_reduce_n<kTiles>(f, rv, scrub);
+            const bool b = (badp >> (rowbit + r)) & 1ull;
+#pragma unroll
+            for (int t = 0; t < kTiles; ++t) frg[r][t] = b ? f[t] : frg[r][t];
           }
         }
       }
@@ -669,11 +760,13 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
         }
         if (++gq == 4) flush_sums();
       }
-      coef_finish<KS>(af, rf, s1, S, D, l, kInv2Pi);
-      if constexpr (kMagic) safe = group_rev_safe<KS>(af, rev_thr);
-      if constexpr (GAIN) {
-        coef_finish<KS>(ax, rx, s1, S, D, l, sx);
-        coef_finish<KS>(ay, ry, s1, S, D, l, sx);
+      if constexpr (!IC) {
+        coef_finish<KS>(af, rf, s1, S, D, l, kInv2Pi);
+        if constexpr (kMagic) safe = group_rev_safe<KS>(af, rev_thr);
+        if constexpr (GAIN) {
+          coef_finish<KS>(ax, rx, s1, S, D, l, sx);
+          coef_finish<KS>(ay, ry, s1, S, D, l, sx);
+        }
       }
     }
     if (sums) flush_sums();
@@ -703,14 +796,16 @@ struct EvalLds {
   static_assert(kRun % 256 == 0 && 16 % NW == 0, "bad LDS eval shape");
 };
 
-template <int KS, int NW, int TPW, bool NT>
+template <int KS, int NW, int TPW, bool NT, bool IC = false>
 __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
     const double* __restrict__ cfrag, const double* __restrict__ coef, int D,
     int ks_real, int64_t S, int64_t P, int64_t n_pb, int64_t n_sc,
     int chunk_groups, float* __restrict__ out, int64_t ring, int64_t ring_base,
     unsigned flags,
-    int sleep, unsigned* __restrict__ sums, double rev_thr) {
+    int sleep, unsigned* __restrict__ sums, double rev_thr, DigArgs dg) {
   using L = EvalLds<NW, TPW>;
+  // IC: the integer-digit contraction (kl_eval_int.h) feeds the same LDS
+  // tile with the same reduced phases as the register tile's IC variant
   __shared__ float tile[2][16][L::kStride];
   // checksums: slot sums of up to 16 groups per half ([half][group % 16]
   // [row]); wave 0 adds a half's 256 consecutive slots with 4 64-lane
@@ -731,14 +826,25 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
     const int64_t wpb = pb * (NW / L::kWavesPerBlock) + wblk;
     const bool live = wpb * kWavePix < P;  // waves past the grid still sync
 
-    double bf[KS][TPW];
+    double bf[IC ? 1 : KS][TPW];
+    if constexpr (!IC) {
 #pragma unroll
-    for (int kk = 0; kk < KS; ++kk)
+      for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+        for (int t = 0; t < TPW; ++t)
+          bf[kk][t] = (live && kk < ks_real)
+                          ? cfrag[((wpb * ks_real + kk) * kTiles + t0 + t) * 64 + l]
+                          : 0.0;
+    }
+    v4i bd[TPW][IC ? kDigits : 1];
+    if constexpr (IC) {
 #pragma unroll
       for (int t = 0; t < TPW; ++t)
-        bf[kk][t] = (live && kk < ks_real)
-                        ? cfrag[((wpb * ks_real + kk) * kTiles + t0 + t) * 64 + l]
-                        : 0.0;
+#pragma unroll
+        for (int i = 0; i < kDigits; ++i)
+          bd[t][i] = live ? dg.cdig[((wpb * kDigits + i) * kTiles + t0 + t) * 64 + l]
+                          : v4i{0, 0, 0, 0};
+    }
 
     const bool scrub = flags & SF_EVAL_NAN_SCRUB;
     const bool be = flags & SF_EVAL_BIG_ENDIAN;
@@ -759,6 +865,60 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
       ng_done = g + 1;
       float(*buf)[L::kStride] = tile[g & 1];
       // ---- contraction: 16 slots x this wave's 64 pixels
+      if constexpr (IC) {
+        // integer digits; rows the digits cannot carry (bit 4 (l >> 4) + r)
+        // take the fp64 contraction, Cpix fragments from memory
+        const int rs = dig_row_slot(l);
+        DigRows wr;
+        dig_load(wr, dg.kdig, s0 + rs, S, l);
+        const int64_t sfl = s0 + rs;
+        const uint8_t fv = dg.kflag[sfl < S ? sfl : S - 1];
+        const unsigned long long bad =
+            __builtin_amdgcn_ballot_w64(!(sfl >= S || fv != 0)) & 0xffffull;
+        float red[4][TPW];
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+          const v4i R = dig_contract(wr, bd[t]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) red[r][t] = (float)R[r] * kTwoM32;
+        }
+        if (bad != 0ull && live) {
+          const int64_t sa = s0 + (l & 15);
+          const double* row = coef + (sa < S ? sa : S - 1) * D;
+          v4d ac[TPW];
+#pragma unroll
+          for (int t = 0; t < TPW; ++t) ac[t] = v4d{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 1
+          for (int kk = 0; kk < ks_real; ++kk) {
+            const int d = 4 * kk + (l >> 4);
+            const double a = keep_if(sa < S && d < D, row[d < D ? d : D - 1] * kInv2Pi);
+#pragma unroll
+            for (int t = 0; t < TPW; ++t)
+              ac[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(
+                  a, cfrag[((wpb * ks_real + kk) * kTiles + t0 + t) * 64 + l], ac[t], 0, 0, 0);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            double rv[TPW];
+            float f[TPW];
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) rv[t] = ac[t][r];
+            rev_reduce_n<TPW>(f, rv, scrub);
+            const bool b = (bad >> (4 * (l >> 4) + r)) & 1ull;
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) red[r][t] = b ? f[t] : red[r][t];
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float* dst = &buf[acc_row(l, r)][wblk * kWavePix + (l & 15) * kTiles + t0];
+          if (TPW == 4)
+            *reinterpret_cast<v4f*>(dst) =
+                v4f{red[r][0], red[r][1 % TPW], red[r][2 % TPW], red[r][3 % TPW]};
+          else
+            *reinterpret_cast<v2f*>(dst) = v2f{red[r][0], red[r][1 % TPW]};
+        }
+      } else {
       double af[KS];
       load_coef<KS>(af, coef, s0, S, D, l, kInv2Pi);
       // fixed-point phase accumulators (kRevMagic) while the REAL k-step
@@ -788,6 +948,7 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
           *reinterpret_cast<v4f*>(dst) = v4f{red[0], red[1], red[2 % TPW], red[3 % TPW]};
         else
           *reinterpret_cast<v2f*>(dst) = v2f{red[0], red[1 % TPW]};
+      }
       }
       for (int z = 0; z < sleep; ++z) __builtin_amdgcn_s_sleep(1);
       __syncthreads();
@@ -959,7 +1120,7 @@ int launch_eval_ks(sf_ctx* ctx, const double* coef,
                      cxb ? cxb + (OFF) * ctx->D : nullptr,                     \
                      cyb ? cyb + (OFF) * ctx->D : nullptr, ctx->D, SL, P, n_pb, \
                      NSC, groups, out, ring, (b + (OFF)) % ring, fl,           \
-                     sb ? sb + (OFF) : nullptr, ctx->d_trash, ctx->rev_thr)
+                     sb ? sb + (OFF) : nullptr, ctx->d_trash, ctx->rev_thr, DigArgs{})
 #define SF_LAUNCH_B(V, F, N, G, B)                                              \
   do {                                                                          \
     if constexpr (KS <= kMagicMaxKS) {                                          \
@@ -1038,7 +1199,7 @@ int launch_eval_shb(sf_ctx* ctx, const double* coef, int64_t S_all,
                      ctx->d_cfrag, cb, nullptr, nullptr, ctx->D, S, P, n_wpb, \
                      n_sc, groups, out, ring, b % ring,                         \
                      flags | eval_band_flags(ctx, n_wpb), sb, ctx->d_trash,     \
-                     ctx->rev_thr)
+                     ctx->rev_thr, DigArgs{})
   if (fast) {
     if (nt) SF_LAUNCH_SHB(true, true); else SF_LAUNCH_SHB(true, false);
   } else {
@@ -1048,6 +1209,56 @@ int launch_eval_shb(sf_ctx* ctx, const double* coef, int64_t S_all,
   SF_HIP(hipGetLastError());
   }
   return SF_OK;
+}
+
+// Does the integer-digit contraction (kl_eval_int.h) serve this call?  Phase
+// screens from D = 45 (below, the fp64 MFMA share of the SIMD is small and
+// the LDS-staged kernels are store-bound already) on the fast epilogue with
+// float4-aligned output; SF_OPT_EVAL_INT = 0 and grids whose |Cpix| does not
+// fit the digits keep the fp64 contraction.
+inline bool eval_int_applies(const sf_ctx* ctx, bool gain, unsigned flags,
+                             bool out_aligned16) {
+  return !gain && ctx->dig_ok && ctx->d_cdig && ctx->eval_int != 0 &&
+         (flags & SF_EVAL_FAST_SINCOS) && ctx->n_pix % 4 == 0 && out_aligned16 &&
+         ctx->ksteps >= 12;
+}
+
+// Slots per launch of the integer contraction: its per-slot digit rows
+// (384 B) live in a context buffer of at most this many slots; launches of
+// 1 M slots are ~0.7 s at 512^2 x D = 50, so the cut costs no measurable tail
+constexpr int64_t kDigChunk = (int64_t)1 << 20;
+
+inline int ensure_kdig(sf_ctx* ctx, int64_t slots) {
+  if (ctx->kdig_slots >= slots) return SF_OK;
+  (void)hipFree(ctx->d_kdig);
+  (void)hipFree(ctx->d_kflag);
+  ctx->d_kdig = nullptr;
+  ctx->d_kflag = nullptr;
+  ctx->kdig_slots = 0;
+  if (hipMalloc(reinterpret_cast<void**>(&ctx->d_kdig), (size_t)slots * kDigits * 64) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&ctx->d_kflag), (size_t)slots) != hipSuccess) {
+    set_error("sf_kl_eval: hipMalloc of the integer-contraction digits failed");
+    return SF_ENOMEM;
+  }
+  ctx->kdig_slots = slots;
+  return SF_OK;
+}
+
+// Prepass of one integer-contraction launch: the digit rows and flags of S
+// slots
+inline int run_kdig(sf_ctx* ctx, const double* cb, int64_t S) {
+  hipLaunchKernelGGL(kl_kdig_kernel<0>, dim3((unsigned)((S + 3) / 4)), dim3(256), 0,
+                     ctx->stream, cb, ctx->D, S, kInv2Pi, ctx->d_kdig, ctx->d_kflag);
+  SF_HIP(hipGetLastError());
+  return SF_OK;
+}
+
+inline DigArgs dig_args(const sf_ctx* ctx, int64_t off) {
+  DigArgs dg;
+  dg.cdig = reinterpret_cast<const v4i*>(ctx->d_cdig);
+  dg.kdig = ctx->d_kdig + off * kDigits * 64;
+  dg.kflag = ctx->d_kflag + off;
+  return dg;
 }
 
 template <int KS, int NW, int TPW>
@@ -1068,13 +1279,28 @@ int launch_eval_lds(sf_ctx* ctx, const double* coef, int64_t S_all,
   const int def_groups = n_pb > 64 ? 16 : KS <= 2 ? 1 : KS <= 5 ? 2 : KS <= 11 ? 4 : 8;
   const int groups = eval_chunk_groups(n_pb, S_all,
                                        ctx->eval_groups ? ctx->eval_groups : def_groups, 1024);
-  const int64_t per = eval_launch_slots(ctx, n_pb, groups, 64 * NW);
+  int64_t per = eval_launch_slots(ctx, n_pb, groups, 64 * NW);
+  // the integer-digit contraction: per-launch slot digits (run_kdig), at
+  // most kDigChunk slots per launch
+  const bool ic = eval_int_applies(ctx, false, flags,
+                                   (reinterpret_cast<uintptr_t>(out) & 15) == 0);
+  if (ic) {
+    const int64_t gs = 16 * (int64_t)groups;
+    const int64_t cap = kDigChunk < gs ? gs : (kDigChunk / gs) * gs;
+    if (per > cap) per = cap;
+    const int rc = ensure_kdig(ctx, S_all < per ? S_all : per);
+    if (rc != SF_OK) return rc;
+  }
   for (int64_t b = 0; b < S_all; b += per) {
   const int64_t S = S_all - b < per ? S_all - b : per;
   const int64_t n_sc = (S + 16 * groups - 1) / (16 * groups);
   const int64_t nblk = eval_grid(ctx, n_pb, n_sc, 64 * NW);
   const double* cb = coef + b * ctx->D;
   unsigned* sb = sums ? sums + b : nullptr;
+  if (ic) {
+    const int rc = run_kdig(ctx, cb, S);
+    if (rc != SF_OK) return rc;
+  }
   // auto XCD map: interleave the pixel blocks over the XCDs when each XCD's
   // contiguous eighth would be <= 8 blocks (measured: 256^2 at 4 KiB runs
   // +2-3 %, 512^2 -3 %; profiles/round1e_eval_xcd_map.txt)
@@ -1082,29 +1308,96 @@ int launch_eval_lds(sf_ctx* ctx, const double* coef, int64_t S_all,
   if (ctx->eval_xcd_map < 0 && (n_pb & 7) == 0 && n_pb / 8 <= 8)
     fl |= kEvalXcdInterleave;
   fl |= eval_band_flags(ctx, n_pb);
-  if (flags & SF_EVAL_NT_STORES)
-    hipLaunchKernelGGL((kl_eval_lds_kernel<KS, NW, TPW, true>), dim3((unsigned)nblk),
-                       dim3(64 * NW), 0, ctx->stream, ctx->d_cfrag, cb, ctx->D,
-                       ctx->ksteps, S, P, n_pb, n_sc, groups, out, ring, b % ring,
-                       fl, ctx->eval_sleep, sb, ctx->rev_thr);
-  else
-    hipLaunchKernelGGL((kl_eval_lds_kernel<KS, NW, TPW, false>), dim3((unsigned)nblk),
-                       dim3(64 * NW), 0, ctx->stream, ctx->d_cfrag, cb, ctx->D,
-                       ctx->ksteps, S, P, n_pb, n_sc, groups, out, ring, b % ring,
-                       fl, ctx->eval_sleep, sb, ctx->rev_thr);
+#define SF_LAUNCH_LDS(N, I)                                                          \
+  hipLaunchKernelGGL((kl_eval_lds_kernel<KS, NW, TPW, N, I>), dim3((unsigned)nblk),     \
+                     dim3(64 * NW), 0, ctx->stream, ctx->d_cfrag, cb, ctx->D,           \
+                     ctx->ksteps, S, P, n_pb, n_sc, groups, out, ring, b % ring, fl,    \
+                     ctx->eval_sleep, sb, ctx->rev_thr, I ? dig_args(ctx, 0) : DigArgs{})
+  // (the integer variant only where it can apply: D >= 45)
+  if (ic) {
+    if constexpr (KS >= 12) {
+      if (flags & SF_EVAL_NT_STORES) SF_LAUNCH_LDS(true, true);
+      else SF_LAUNCH_LDS(false, true);
+    }
+  } else {
+    if (flags & SF_EVAL_NT_STORES) SF_LAUNCH_LDS(true, false);
+    else SF_LAUNCH_LDS(false, false);
+  }
+#undef SF_LAUNCH_LDS
   SF_HIP(hipGetLastError());
   }
   return SF_OK;
 }
 
+// The register tile on the integer-digit contraction (phase, D >= 45)
+template <int KS>
+int launch_eval_int(sf_ctx* ctx, const double* coef, int64_t S_all, float* out,
+                    int64_t ring, unsigned flags, unsigned* sums) {
+  const int64_t P = ctx->n_pix;
+  const int64_t n_pb = ctx->n_pix_blocks;
+  // large grids (>= 1024 blocks of 256 px: 512^2 and up): items of 4 groups
+  // (the digit fragments are 6 KB per wave block, a quarter of the fp64 ones,
+  // so short items cost little reload): 512^2 x D = 50 0.691 (64 groups) ->
+  // 0.744 of 8 TB/s, 2 / 8 groups 0.723 / 0.731
+  // (profiles/round3y_eval_items_512.txt)
+  const int def_groups = n_pb >= 1024 ? 4 : 64;
+  const int groups = eval_chunk_groups(n_pb, S_all, ctx->eval_groups ? ctx->eval_groups : def_groups, 2048);
+  const int64_t gs = 16 * (int64_t)groups;
+  int64_t per = eval_launch_slots(ctx, n_pb, groups, 256);
+  const int64_t cap = kDigChunk < gs ? gs : (kDigChunk / gs) * gs;
+  if (per > cap) per = cap;
+  {
+    const int rc = ensure_kdig(ctx, S_all < per ? S_all : per);
+    if (rc != SF_OK) return rc;
+  }
+  // bands / XCD map as the fp64 register tile (launch_eval_ks)
+  const int auto_bands = n_pb >= 1024 ? (int)(n_pb / 128 < 128 ? n_pb / 128 : 128) : 1;
+  unsigned fl = flags | eval_band_flags(ctx, n_pb, auto_bands);
+  if (ctx->eval_xcd_map < 0 && ctx->eval_bands == 0 && auto_bands > 1)
+    fl |= kEvalXcdInterleave;
+  const bool nt = flags & SF_EVAL_NT_STORES;
+  const bool be = flags & SF_EVAL_BIG_ENDIAN;
+  for (int64_t b = 0; b < S_all; b += per) {
+    const int64_t S = S_all - b < per ? S_all - b : per;
+    const double* cb = coef + b * ctx->D;
+    unsigned* sb = sums ? sums + b : nullptr;
+    {
+      const int rc = run_kdig(ctx, cb, S);
+      if (rc != SF_OK) return rc;
+    }
+    // (direct addressing: measured 2 % slower at D = 50 with fp64, not used)
+    const int64_t nsc = (S + gs - 1) / gs;
+    const unsigned nblk = (unsigned)eval_grid(ctx, n_pb, nsc, 256);
+#define SF_LAUNCH_IC(N, B)                                                          \
+  hipLaunchKernelGGL((kl_eval_kernel<KS, 2, true, true, N, false, false, B, false, true>), \
+                     dim3(nblk), dim3(256), 0, ctx->stream, ctx->d_cfrag, cb, nullptr,     \
+                     nullptr, ctx->D, S, P, n_pb, nsc, groups, out, ring, b % ring, fl,    \
+                     sb, ctx->d_trash, ctx->rev_thr, dig_args(ctx, 0))
+    if constexpr (KS >= 12) {
+      if (nt) {
+        if (be) SF_LAUNCH_IC(true, 1); else SF_LAUNCH_IC(true, 0);
+      } else {
+        if (be) SF_LAUNCH_IC(false, 1); else SF_LAUNCH_IC(false, 0);
+      }
+    }
+#undef SF_LAUNCH_IC
+    SF_HIP(hipGetLastError());
+  }
+  return SF_OK;
+}
 
 template <int KS>
 int launch_eval_pick(sf_ctx* ctx, const double* coef, const double* cxx,
                             const double* cyy, int64_t S, float* out,
                             int64_t ring, unsigned flags,
                             unsigned* sums) {
-  const int v = pick_eval_kernel(ctx, cxx != nullptr, flags,
-                                 (reinterpret_cast<uintptr_t>(out) & 15) == 0);
+  const bool aligned = (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+  const int v = pick_eval_kernel(ctx, cxx != nullptr, flags, aligned);
+  // the integer-digit contraction: the LDS-staged kernels take it themselves,
+  // the register tile through launch_eval_int
+  if (eval_int_applies(ctx, cxx != nullptr, flags, aligned) &&
+      (v == SF_EVAL_KERNEL_TILE || v == SF_EVAL_KERNEL_TILE3))
+    return launch_eval_int<KS>(ctx, coef, S, out, ring, flags, sums);
   switch (v) {
     case SF_EVAL_KERNEL_LDS4:
       return launch_eval_lds<KS, 4, 4>(ctx, coef, S, out, ring, flags, sums);

@@ -36,6 +36,10 @@ constexpr int kWavePix = 16 * kTiles;           // 64 consecutive pixels per wav
 constexpr int kEvalWaves = 4;                   // waves per workgroup
 constexpr int kBlockPix = kWavePix * kEvalWaves; // 256 pixels per workgroup
 
+// integer-digit contraction (kl_eval_int.h): balanced base-256 digits per
+// operand
+constexpr int kDigits = 6;
+
 }  // namespace sf
 
 struct sf_ctx {
@@ -59,6 +63,16 @@ struct sf_ctx {
   // fixed-point phase epilogue: a lane's |coef| sum (turns) below rev_thr
   // bounds its phases below 2^17 turns (kl_eval_impl.h group_rev_safe)
   double rev_thr = 0.0;
+  // integer-digit contraction (kl_eval_int.h): Cpix as 6 balanced base-256
+  // digits of rint(Cpix * 2^36) in i8 MFMA B-fragment order (phase screens,
+  // D >= 45), and whether the grid fits the digits
+  int8_t* d_cdig = nullptr;    // [wave pixel blocks][6][kTiles][64][16 B]
+  int dig_ok = 0;              // 1: max |Cpix| * 2^36 fits 6 digits
+  int eval_int = -1;           // SF_OPT_EVAL_INT (-1 auto, 0 off)
+  // per-call slot digits of the integer contraction (kl_kdig_kernel)
+  int8_t* d_kdig = nullptr;    // [slot][6][64]
+  uint8_t* d_kflag = nullptr;  // [slot]: 1 = integer path
+  int64_t kdig_slots = 0;      // slots the buffers hold
   double h_pp[3 * SF_MAX_DIR] = {};  // host copy of the piercepoints
   // fit scratch
   uint8_t* d_skip = nullptr;   // [F][A] block skip flags
@@ -127,6 +141,7 @@ int launch_fit_general(sf_ctx* ctx, const int* slot_list, const int* n_list,
                        double* resid, float* w_out, int32_t* order_out);
 int launch_basis(sf_ctx* ctx);
 int launch_cpix(sf_ctx* ctx, const double* d_x, const double* d_y);
+int launch_cdig(sf_ctx* ctx, const double* d_x, const double* d_y);
 int launch_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,
                int F, int A, const sf_fit_params* p, double* coef,
                double* resid, float* w_out, int32_t* order_out);

@@ -1,0 +1,126 @@
+"""The integer-digit evaluation contraction (kl_eval_int.h, SF_OPT_EVAL_INT).
+
+Phase screens with D >= 45 evaluate Cpix . coef on i8 MFMAs over 6 balanced
+base-256 digits of 36- / 44-bit fixed point, exactly modulo 2^32 turns
+(kl_screen.py:444-449 contraction, :367-380 epilogue).  Checked here against
+the oracle (fp64 numpy restatement of calculate_kl_screen) and against the
+fp64 MFMA contraction of the same library (SF_OPT_EVAL_INT = 0):
+
+* finite slots: |d| <= 2e-6 vs the oracle (the fast-epilogue tolerance of
+  every evaluation test), <= 3e-7 vs the fp64 contraction (phase error
+  <= 2^-28 turn plus one fp32 rounding of the reduced phase either way);
+* slots the digits cannot carry (NaN / Inf, |coef / 2 pi| beyond ~7.9 turns)
+  take the fp64 contraction inside the same launch: bit for bit the fp64
+  register tile's output;
+* every kernel (register tile, LDS-staged) writes the same bits with it;
+* the path really runs: some values differ in the last bits from the fp64
+  contraction.
+Needs an MI355X: every test is marked ``gpu``.
+"""
+
+import numpy as np
+import pytest
+
+from conftest import FIELD
+from oracle import kl as okl
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def ctx(dev):
+    from ska_sdp_screen_fitting_amd import get_context
+    c = get_context(0)
+    c.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    return c
+
+
+def grid_for(n_dir, grid, seed):
+    from ska_sdp_screen_fitting_amd import geometry
+    from ska_sdp_screen_fitting_amd.synthetic import make_solutions
+    s = make_solutions(n_ant=2, n_time=2, n_freq=1, n_dir=n_dir, seed=seed)
+    pp, mra, mdec = geometry.piercepoints(s.dir_radec)
+    cell = FIELD["width"] / (grid - 0.5)
+    x, y = geometry.grid_coords(FIELD["rad"], FIELD["dec"], FIELD["width"],
+                                cell, mra, mdec)
+    return pp, x, y
+
+
+def run(ctx, dev, coefs, S, grid, int_on, flags, gain=False):
+    from ska_sdp_screen_fitting_amd._lib import SF_OPT_EVAL_INT
+    ctx.set_option(SF_OPT_EVAL_INT, -1 if int_on else 0)
+    try:
+        cs = [torch.from_numpy(np.ascontiguousarray(c, np.float64)).to(dev) for c in coefs]
+        out = torch.full((S, 4, grid, grid), -7.0, dtype=torch.float32, device=dev)
+        if gain:
+            ctx.eval_gain(cs[0], cs[1], cs[2], S, out, flags=flags)
+        else:
+            ctx.eval(cs[0], S, out, flags=flags)
+        torch.cuda.synchronize()
+        return out.cpu().numpy()
+    finally:
+        ctx.set_option(SF_OPT_EVAL_INT, -1)
+
+
+@pytest.mark.parametrize("n_dir,grid", [(50, 64), (45, 128), (60, 96)])
+def test_int_phase_vs_fp64_and_oracle(ctx, dev, n_dir, grid):
+    from ska_sdp_screen_fitting_amd._lib import (
+        EVAL_KERNEL_NAMES, SF_EVAL_FAST_SINCOS, SF_EVAL_KERNEL_AUTO,
+        SF_EVAL_KERNEL_SHB, SF_EVAL_KERNEL_TILE, SF_OPT_EVAL_KERNEL)
+    pp, x, y = grid_for(n_dir, grid, seed=n_dir)
+    ctx.set_basis(pp)
+    ctx.set_grid(x, y)
+    rng = np.random.default_rng(grid + n_dir)
+    S = 45  # ragged: two whole 16-slot groups and a tail
+    coef = rng.normal(0, 0.01, size=(S, n_dir))
+    coef[20:30] *= 300.0                 # up to ~1.6 turns per coefficient
+    coef[3, 1] = 2 * np.pi * 9.0         # 9 turns: past the digit range
+    coef[9, n_dir // 2] = np.nan
+    coef[31, 0] = np.inf
+    fb = [3, 9, 31]                      # the fp64 rows
+    flags = 1 | SF_EVAL_FAST_SINCOS
+    # auto: the register tile; SHB (fp64 fragments in LDS) is replaced by it;
+    # the LDS-staged kernels take the integer contraction too -- every kernel
+    # writes the same bits (below)
+    try:
+        assert ctx.eval_kernel(flags) == "kl_eval_kernel"
+        ctx.set_option(SF_OPT_EVAL_KERNEL, SF_EVAL_KERNEL_SHB)
+        assert ctx.eval_kernel(flags) == "kl_eval_kernel"
+    finally:
+        ctx.set_option(SF_OPT_EVAL_KERNEL, SF_EVAL_KERNEL_AUTO)
+    oi = run(ctx, dev, [coef], S, grid, True, flags)
+    try:
+        for kv in sorted(EVAL_KERNEL_NAMES):
+            ctx.set_option(SF_OPT_EVAL_KERNEL, kv)
+            o = run(ctx, dev, [coef], S, grid, True, flags)
+            assert np.array_equal(o.view(np.int32), oi.view(np.int32)), kv
+    finally:
+        ctx.set_option(SF_OPT_EVAL_KERNEL, SF_EVAL_KERNEL_AUTO)
+    try:
+        ctx.set_option(SF_OPT_EVAL_KERNEL, SF_EVAL_KERNEL_TILE)
+        of = run(ctx, dev, [coef], S, grid, False, flags)
+    finally:
+        ctx.set_option(SF_OPT_EVAL_KERNEL, SF_EVAL_KERNEL_AUTO)
+    assert np.array_equal(oi[fb].view(np.int32), of[fb].view(np.int32))
+    assert np.all(oi[[9, 31], 0::2] == 1.0) and np.all(oi[[9, 31], 1::2] == 0.0)
+    good = [s for s in range(S) if s not in fb]
+    np.testing.assert_allclose(oi[good], of[good], rtol=0, atol=3e-7)
+    assert not np.array_equal(oi[good].view(np.int32), of[good].view(np.int32))
+    cpix = okl.cpix_matrix(pp, x, y)
+    ok = np.isfinite(coef).all(axis=1)
+    want = okl.eval_planes(okl.eval_phase_screens(coef[ok], cpix))
+    np.testing.assert_allclose(oi[ok].reshape(want.shape), want, rtol=0, atol=2e-6)
+    # unscrubbed: the NaN / Inf rows stay NaN, the rest is unchanged
+    on = run(ctx, dev, [coef], S, grid, True, SF_EVAL_FAST_SINCOS)
+    assert np.isnan(on[[9, 31]]).all()
+    on[[9, 31]] = oi[[9, 31]]
+    assert np.array_equal(on.view(np.int32), oi.view(np.int32))
