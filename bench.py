@@ -98,7 +98,7 @@ def parse():
                          "pixel blocks per XCD, 1 interleaved")
     ap.add_argument("--eval-int", type=int, default=-1, choices=(-1, 0),
                     help="SF_OPT_EVAL_INT: -1 the integer-digit contraction where "
-                         "it applies (phase D >= 45, gain screens), 0 fp64 MFMAs")
+                         "it applies (phase screens, D >= 45), 0 fp64 MFMAs")
     ap.add_argument("--eval-groups", type=int, default=0,
                     help="SF_OPT_EVAL_GROUPS: most 16-slot groups per eval work "
                          "item (0 = library default)")
@@ -458,6 +458,7 @@ def dist_block(args, world, record):
 
 
 FP64_MFMA_PEAK_TFS = 78.6  # MI355X fp64 matrix peak (AMD spec, dense)
+I8_MFMA_PEAK_TOPS = 5000.0  # MI355X int8 matrix peak (dense; 2x bf16)
 
 
 def _profile_entry(name, workload, kernel):
@@ -475,20 +476,32 @@ def _profile_entry(name, workload, kernel):
     return None
 
 
-def mfma_line(kernel, launch_slots, P, D, launch_s, workload, n_contract=1):
-    """fp64 MFMA work of one evaluation launch: executed flops (the k-steps
-    padded to a multiple of 4 directions) and the algorithmic 2 D flops per
-    pixel per slot, over the launch time, against the fp64 matrix peak; the
-    MFMA-busy fraction from PMC counters when profiles/mfma.json holds this
-    workload."""
+def mfma_line(kernel, launch_slots, P, D, launch_s, workload, n_contract=1,
+              contraction="f64"):
+    """MFMA work of one evaluation launch over the launch time.  fp64
+    contraction: executed flops (the k-steps padded to a multiple of 4
+    directions) against the fp64 matrix peak; integer-digit contraction
+    (kl_eval_int.h): 25 v_mfma_i32_16x16x64_i8 per 16 slots x 16 pixels
+    (2 x 16 x 16 x 64 ops each) against the int8 matrix peak.  Both carry the
+    algorithmic 2 D flops per pixel per slot; the MFMA-busy fraction from PMC
+    counters when profiles/mfma.json holds this workload."""
     ks = (D + 3) // 4
-    executed = launch_slots * P * 2.0 * 4 * ks * n_contract
     algo = launch_slots * P * 2.0 * D * n_contract
-    res = {"kernel": kernel, "unit": "TFLOP/s", "peak": FP64_MFMA_PEAK_TFS,
-           "executed": executed / launch_s / 1e12,
-           "algorithmic": algo / launch_s / 1e12,
-           "flops_per_launch": executed}
-    res["frac"] = res["executed"] / FP64_MFMA_PEAK_TFS
+    if contraction == "i8-digits":
+        executed = launch_slots * P * 25 * 2.0 * 64 * n_contract
+        res = {"kernel": kernel, "contraction": contraction, "unit": "TOP/s (i8)",
+               "peak": I8_MFMA_PEAK_TOPS, "executed": executed / launch_s / 1e12,
+               "algorithmic_fp64_equiv_tflops": algo / launch_s / 1e12,
+               "ops_per_launch": executed}
+        res["frac"] = res["executed"] / I8_MFMA_PEAK_TOPS
+    else:
+        executed = launch_slots * P * 2.0 * 4 * ks * n_contract
+        res = {"kernel": kernel, "contraction": contraction, "unit": "TFLOP/s",
+               "peak": FP64_MFMA_PEAK_TFS,
+               "executed": executed / launch_s / 1e12,
+               "algorithmic": algo / launch_s / 1e12,
+               "flops_per_launch": executed}
+        res["frac"] = res["executed"] / FP64_MFMA_PEAK_TFS
     e = _profile_entry("mfma.json", workload, kernel)
     if e is not None:
         res["busy_frac_pmc"] = e.get("mfma_busy_frac")
@@ -847,6 +860,7 @@ def main():
     ctx.set_option(SF_OPT_EVAL_GROUPS, args.eval_groups)
     ctx.set_option(SF_OPT_EVAL_INT, args.eval_int)
     eval_kernel_name = ctx.eval_kernel(flags, gain=gain)
+    contraction = ctx.eval_contraction(flags, gain=gain)
     # discard + checksum mode: the cubes go
     # through the HBM ring and every slot's checksum is accumulated
     checksum = args.checksum == "on" or (args.checksum == "auto"
@@ -1013,7 +1027,10 @@ def main():
             "higher_is_better": True,
             "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
-            "dtype": "f64",
+            # the arithmetic of the contraction: fp64 MFMAs, or (phase, D >=
+            # 45) exact int8-digit products of 36- / 44-bit fixed point into
+            # int32 modulo 2^32 turns; the fit is fp64 either way
+            "dtype": "f64" if contraction == "f64" else "i8-digit fixed point (f64 in)",
             "data": "synthetic",
             "config": {
                 "workload": (f"{args.workload}{'-gain' if gain else ''}: {A_total} ant x "
@@ -1044,7 +1061,7 @@ def main():
                 "frac_of_box_store_ceiling": achieved / ceil["GBs"] if ceil else None,
             },
             "mfma": mfma_line(eval_kernel_name, S / n_chunks, P, D,
-                              t_eval_launch, wkey, 3 if gain else 1),
+                              t_eval_launch, wkey, 3 if gain else 1, contraction),
             "stages_ms": {"fit": t_fit * 1e3, "eval": t_eval * 1e3,
                           "overlap": "fit(c+1) || eval(c), %d time chunks" % n_chunks
                           if n_chunks > 1 else "none"},

@@ -171,12 +171,13 @@ int sf_device_cus(sf_ctx* ctx, int* n_cu);
  * -1 (default): the integer-digit contraction -- Cpix and the coefficients
  * as 6 balanced base-256 digits of 36- / 44-bit fixed point, contracted
  * exactly on i8 MFMAs (64x the fp64 MFMA rate per product) modulo 2^32
- * turns -- for phase screens with D >= 45 and for gain screens, on the fast
- * (hardware sincos) epilogue with float4-aligned output; slots whose
+ * turns -- for phase screens with D >= 45, on the fast (hardware sincos)
+ * epilogue with float4-aligned output (gain screens keep fp64); slots whose
  * coefficients are not finite or out of the digit range take the fp64
  * contraction.  |error| <= 2^-28 turn of phase (2^-32 typical), below the
- * fp32 rounding of the reduced phase; while it applies every kernel request
- * runs the register tile (sf_get_eval_kernel says so). */
+ * fp32 rounding of the reduced phase; it runs in the register tile and the
+ * LDS-staged kernels alike (same bits), SF_EVAL_KERNEL_SHB is replaced by the
+ * register tile (sf_get_eval_kernel / sf_get_eval_contraction say so). */
 #define SF_OPT_EVAL_INT 15
 #define SF_EVAL_KERNEL_AUTO 0
 #define SF_EVAL_KERNEL_TILE 1
@@ -191,6 +192,12 @@ int sf_device_cus(sf_ctx* ctx, int* n_cu);
  * runs for the current grid and these flags on a 16-byte aligned output
  * (one of SF_EVAL_KERNEL_TILE / _LDS4 / _LDS8 / _LDS16). */
 int sf_get_eval_kernel(sf_ctx* ctx, int gain, unsigned flags, int* kernel);
+/* The contraction of that evaluation: SF_EVAL_CONTRACTION_F64 (fp64 MFMAs) or
+ * SF_EVAL_CONTRACTION_I8_DIGITS (the integer-digit contraction,
+ * SF_OPT_EVAL_INT). */
+#define SF_EVAL_CONTRACTION_F64 0
+#define SF_EVAL_CONTRACTION_I8_DIGITS 1
+int sf_get_eval_contraction(sf_ctx* ctx, int gain, unsigned flags, int* contraction);
 int sf_set_option(sf_ctx* ctx, int option, int value);
 int sf_alloc(sf_ctx* ctx, size_t bytes, void** dev_ptr);
 int sf_free(sf_ctx* ctx, void* dev_ptr);

@@ -244,6 +244,16 @@ int sf_get_eval_kernel(sf_ctx* ctx, int gain, unsigned flags, int* kernel) {
   return SF_OK;
 }
 
+int sf_get_eval_contraction(sf_ctx* ctx, int gain, unsigned flags, int* contraction) {
+  SF_REQUIRE(ctx && contraction, SF_EINVAL, "sf_get_eval_contraction: bad argument");
+  SF_REQUIRE(ctx->ksteps > 0, SF_EINVAL,
+             "sf_get_eval_contraction: call sf_set_grid first");
+  *contraction = sf::eval_int_applies(ctx, gain != 0, flags, true)
+                     ? SF_EVAL_CONTRACTION_I8_DIGITS
+                     : SF_EVAL_CONTRACTION_F64;
+  return SF_OK;
+}
+
 int sf_synchronize(sf_ctx* ctx) {
   SF_REQUIRE(ctx, SF_EINVAL, "sf_synchronize: NULL context");
   SF_HIP(hipSetDevice(ctx->device));

@@ -1211,18 +1211,6 @@ int launch_eval_shb(sf_ctx* ctx, const double* coef, int64_t S_all,
   return SF_OK;
 }
 
-// Does the integer-digit contraction (kl_eval_int.h) serve this call?  Phase
-// screens from D = 45 (below, the fp64 MFMA share of the SIMD is small and
-// the LDS-staged kernels are store-bound already) on the fast epilogue with
-// float4-aligned output; SF_OPT_EVAL_INT = 0 and grids whose |Cpix| does not
-// fit the digits keep the fp64 contraction.
-inline bool eval_int_applies(const sf_ctx* ctx, bool gain, unsigned flags,
-                             bool out_aligned16) {
-  return !gain && ctx->dig_ok && ctx->d_cdig && ctx->eval_int != 0 &&
-         (flags & SF_EVAL_FAST_SINCOS) && ctx->n_pix % 4 == 0 && out_aligned16 &&
-         ctx->ksteps >= 12;
-}
-
 // Slots per launch of the integer contraction: its per-slot digit rows
 // (384 B) live in a context buffer of at most this many slots; launches of
 // 1 M slots are ~0.7 s at 512^2 x D = 50, so the cut costs no measurable tail

@@ -126,6 +126,18 @@ struct sf_ctx {
 };
 
 namespace sf {
+// Does the integer-digit contraction (kl_eval_int.h) serve this call?  Phase
+// screens from D = 45 (below, the fp64 MFMA share of the SIMD is small and
+// the LDS-staged kernels are store-bound already) on the fast epilogue with
+// float4-aligned output; SF_OPT_EVAL_INT = 0 and grids whose |Cpix| does not
+// fit the digits keep the fp64 contraction.
+inline bool eval_int_applies(const sf_ctx* ctx, bool gain, unsigned flags,
+                             bool out_aligned16) {
+  return !gain && ctx->dig_ok && ctx->d_cdig && ctx->eval_int != 0 &&
+         (flags & SF_EVAL_FAST_SINCOS) && ctx->n_pix % 4 == 0 && out_aligned16 &&
+         ctx->ksteps >= 12;
+}
+
 struct RefSpec {
   int sub = -1;                 // local station whose phases are subtracted
   const double* refph = nullptr;  // or: external reference phases [T][F][D]

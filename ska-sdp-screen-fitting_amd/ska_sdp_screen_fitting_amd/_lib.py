@@ -57,7 +57,7 @@ EVAL_KERNEL_NAMES = {SF_EVAL_KERNEL_TILE: "kl_eval_kernel",
 # every symbol include/screenfit.h declares (checked by tests/test_capi.py)
 EXPORTED = (
     "sf_version", "sf_last_error", "sf_create", "sf_destroy", "sf_set_stream",
-    "sf_synchronize", "sf_set_option", "sf_get_eval_kernel", "sf_alloc", "sf_free", "sf_copy_h2d", "sf_copy_d2h",
+    "sf_synchronize", "sf_set_option", "sf_get_eval_kernel", "sf_get_eval_contraction", "sf_alloc", "sf_free", "sf_copy_h2d", "sf_copy_d2h",
     "sf_set_basis", "sf_get_basis", "sf_kl_fit", "sf_get_fit_stats",
     "sf_stream_create", "sf_stream_destroy", "sf_device_cus",
     "sf_set_grid", "sf_kl_eval", "sf_kl_eval_gain", "sf_kl_eval_sums",
@@ -105,6 +105,7 @@ def load_library(path=None):
             "sf_synchronize": ([vp], c_int),
             "sf_set_option": ([vp, c_int, c_int], c_int),
             "sf_get_eval_kernel": ([vp, c_int, ctypes.c_uint, ip], c_int),
+            "sf_get_eval_contraction": ([vp, c_int, ctypes.c_uint, ip], c_int),
             "sf_alloc": ([vp, ctypes.c_size_t, ctypes.POINTER(vp)], c_int),
             "sf_free": ([vp, vp], c_int),
             "sf_copy_h2d": ([vp, vp, vp, ctypes.c_size_t], c_int),
@@ -210,6 +211,14 @@ class Context:
         _check(self.lib.sf_get_eval_kernel(self.h, int(bool(gain)), int(flags),
                                            ctypes.byref(k)), "sf_get_eval_kernel")
         return EVAL_KERNEL_NAMES[k.value]
+
+    def eval_contraction(self, flags, gain=False):
+        """'f64' (fp64 MFMAs) or 'i8-digits' (the integer-digit contraction)
+        for the evaluation sf_kl_eval runs with these flags."""
+        k = ctypes.c_int()
+        _check(self.lib.sf_get_eval_contraction(self.h, int(bool(gain)), int(flags),
+                                                ctypes.byref(k)), "sf_get_eval_contraction")
+        return "i8-digits" if k.value == 1 else "f64"
 
     def synchronize(self):
         _check(self.lib.sf_synchronize(self.h), "sf_synchronize")
