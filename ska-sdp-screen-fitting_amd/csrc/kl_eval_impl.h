@@ -1082,12 +1082,10 @@ int launch_eval_ks(sf_ctx* ctx, const double* coef,
                           unsigned* sums) {
   const int64_t P = ctx->n_pix;
   const int64_t n_pb = ctx->n_pix_blocks;
-  // large grids (>= 1024 blocks of 256 px: 512^2 and up): items of 8 groups
-  // (512^2 x D = 50: 0.691 with 64 -> 0.725 of 8 TB/s with 8, 0.676 with 4:
-  // the 26 KB of fp64 Cpix fragments a wave block reloads per item;
-  // profiles/round3y_eval_items_512.txt)
-  const int def_groups = n_pb >= 1024 ? 8 : 64;
-  const int groups = eval_chunk_groups(n_pb, S_all, ctx->eval_groups ? ctx->eval_groups : def_groups, 2048);
+  // (64 groups also at 512^2: 8 measured 0.725 vs 0.691 of 8 TB/s in
+  // tools/eval_variants.py but 0.703 vs 0.714 in the config-5 bench step,
+  // profiles/round3y_eval_items_512.txt, round3ad_c5_fp64_g8.json)
+  const int groups = eval_chunk_groups(n_pb, S_all, ctx->eval_groups ? ctx->eval_groups : 64, 2048);
   const int64_t per = eval_launch_slots(ctx, n_pb, groups, 256);
   // large grids (>= 1024 blocks of 256 px: 512^2 and up): auto bands of 128
   // blocks with the XCD-interleaved map -- 512^2 x D = 50 0.706 -> 0.732 of
