@@ -124,3 +124,67 @@ def test_int_phase_vs_fp64_and_oracle(ctx, dev, n_dir, grid):
     assert np.isnan(on[[9, 31]]).all()
     on[[9, 31]] = oi[[9, 31]]
     assert np.array_equal(on.view(np.int32), oi.view(np.int32))
+
+
+def test_int_grid_out_of_digit_range_keeps_fp64(ctx, dev):
+    """A grid whose |Cpix| exceeds the 36-bit digits (piercepoints ~1e5 TAN
+    pixels away: |Cpix| ~ 1e4 > 2^10.9) keeps the fp64 contraction for the
+    whole call, and still matches the oracle."""
+    from ska_sdp_screen_fitting_amd._lib import SF_EVAL_FAST_SINCOS, SF_OPT_EVAL_INT
+    rng = np.random.default_rng(3)
+    D, grid = 48, 32
+    pp = np.stack([rng.uniform(-1e5, 1e5, D), rng.uniform(-1e5, 1e5, D), np.zeros(D)], 1)
+    x = np.linspace(-500.0, 500.0, grid)
+    ctx.set_basis(pp)
+    ctx.set_grid(x, x)
+    flags = 1 | SF_EVAL_FAST_SINCOS
+    assert ctx.eval_contraction(flags) == "f64"
+    coef = rng.normal(0, 1e-4, size=(19, D))
+    oi = run(ctx, dev, [coef], 19, grid, True, flags)
+    of = run(ctx, dev, [coef], 19, grid, False, flags)
+    assert np.array_equal(oi.view(np.int32), of.view(np.int32))
+    cpix = okl.cpix_matrix(pp, x, x)
+    assert np.abs(cpix).max() > 2 ** 11
+    want = okl.eval_planes(okl.eval_phase_screens(coef, cpix))
+    np.testing.assert_allclose(oi.reshape(want.shape), want, rtol=0, atol=2e-6)
+    # an ordinary grid of the same D does take the integer contraction
+    pp2, x2, y2 = grid_for(D, 64, seed=9)
+    ctx.set_basis(pp2)
+    ctx.set_grid(x2, y2)
+    assert ctx.eval_contraction(flags) == "i8-digits"
+    ctx.set_option(SF_OPT_EVAL_INT, 0)
+    try:
+        assert ctx.eval_contraction(flags) == "f64"
+    finally:
+        ctx.set_option(SF_OPT_EVAL_INT, -1)
+
+
+def test_int_many_launches_checksums(ctx, dev):
+    """A call of more slots than one integer launch holds (1 M slot digit
+    buffer): 1.1 M slots into a 32-slot ring in checksum mode; the sums of the
+    last slots (second launch) equal those of the same slots evaluated alone,
+    and the first slots' likewise."""
+    from ska_sdp_screen_fitting_amd._lib import SF_EVAL_FAST_SINCOS, SF_EVAL_NAN_SCRUB
+    D, grid = 50, 32
+    pp, x, y = grid_for(D, grid, seed=11)
+    ctx.set_basis(pp)
+    ctx.set_grid(x, y)
+    flags = SF_EVAL_NAN_SCRUB | SF_EVAL_FAST_SINCOS
+    assert ctx.eval_contraction(flags) == "i8-digits"
+    S = 1_100_000
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    coef = torch.randn((S, D), generator=g, device=dev, dtype=torch.float64) * 0.01
+    coef[S - 7, 3] = float("nan")
+    ring = 32
+    out = torch.empty((ring, 4, grid, grid), dtype=torch.float32, device=dev)
+    sums = torch.zeros(S, dtype=torch.int32, device=dev)
+    ctx.eval_sums(coef, S, out, sums, ring, flags=flags)
+    torch.cuda.synchronize()
+    for a, b in ((0, 40), (S - 40, S)):
+        part = coef[a:b].contiguous()
+        o = torch.empty((b - a, 4, grid, grid), dtype=torch.float32, device=dev)
+        s2 = torch.zeros(b - a, dtype=torch.int32, device=dev)
+        ctx.eval_sums(part, b - a, o, s2, b - a, flags=flags)
+        torch.cuda.synchronize()
+        assert torch.equal(s2, sums[a:b]), (a, b)
