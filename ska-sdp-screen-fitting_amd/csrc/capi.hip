@@ -453,10 +453,12 @@ int sf_set_grid(sf_ctx* ctx, const double* x, int nx, const double* y,
   ctx->dig_ok = 0;
   if (rc == SF_OK && ctx->ksteps >= 12 && std::isfinite(cmax) &&
       cmax * 68719476736.0 < std::ldexp(1.0, 46) * 1.86) {
-    rc = dev_alloc(&ctx->d_cdig, (size_t)ctx->n_pix_blocks * sf::kEvalWaves *
-                                     sf::kDigits * sf::kTiles * 64 * 16);
-    if (rc == SF_OK) rc = sf::launch_cdig(ctx, dx, dy);
-    if (rc == SF_OK) ctx->dig_ok = 1;
+    // (no memory for the digits: the fp64 contraction serves, not an error)
+    if (dev_alloc(&ctx->d_cdig, (size_t)ctx->n_pix_blocks * sf::kEvalWaves *
+                                    sf::kDigits * sf::kTiles * 64 * 16) == SF_OK) {
+      rc = sf::launch_cdig(ctx, dx, dy);
+      if (rc == SF_OK) ctx->dig_ok = 1;
+    }
   }
   if (hipStreamSynchronize(ctx->stream) != hipSuccess && rc == SF_OK) {
     set_error("sf_set_grid: pixel basis kernel failed");
