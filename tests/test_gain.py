@@ -200,6 +200,75 @@ def test_gain_eval_vs_reference(gain, fast):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fast", [False, True])
+def test_gain_eval_finite_groups_and_scrub(gain, fast):
+    """The fast epilogue skips the per-value NaN check of a 16-slot group
+    whose coefficient sums prove every value finite (kl_eval_impl.h
+    group_amp_finite): groups below that bound, above it (|log2 A| up to 30,
+    finite), with a NaN amplitude or phase coefficient (scrubbed to 1 / 0),
+    against fp64 numpy; and a group's bits do not depend on which of the two
+    paths it took."""
+    from ska_sdp_screen_fitting_amd._lib import (SF_EVAL_FAST_SINCOS,
+                                                 SF_EVAL_NAN_SCRUB)
+    torch, dev = _torch_dev()
+    ctx = _ctx(torch, dev)
+    g = gain
+    pp = g["piercepoints"]
+    ctx.set_basis(pp)
+    ctx.set_grid(g["x17"], g["y17"])
+    cpix = okl.cpix_matrix(pp, g["x17"], g["y17"])
+    D = cpix.shape[1]
+    cmax = np.abs(cpix).max()
+    L = np.log2(10.0)
+    rng = np.random.default_rng(11)
+    S = 53
+    ph = rng.normal(0, 0.01, (S, D))
+    amp = [rng.normal(0, 1.0, (S, D)) for _ in range(2)]
+    for a in amp:
+        # groups 0, 2, 3: sum |coef| log2(10) max|Cpix| = 20 (finite bound)
+        a *= 20.0 / (np.abs(a).sum(1, keepdims=True) * L * cmax)
+        # group 1: |log2 A| reaches 30, past the bound (finite values)
+        big = a[16:32] * (30.0 / np.abs(a[16:32] @ cpix.T * L).max(1, keepdims=True))
+        assert np.all(np.abs(big).sum(1) * L * cmax > 128.0)
+        a[16:32] = big
+    amp[0][35, 2] = np.nan
+    ph[50, 1] = np.nan
+    flags = SF_EVAL_NAN_SCRUB | (SF_EVAL_FAST_SINCOS if fast else 0)
+
+    def run(p, ax, ay):
+        up = [torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (p, ax, ay)]
+        n = p.shape[0]
+        out = torch.full((n, 4, 17, 17), -7.0, dtype=torch.float32, device=dev)
+        ctx.eval_gain(up[0], up[1], up[2], n, out, n, flags)
+        torch.cuda.synchronize()
+        return out.cpu().numpy().reshape(n, 4, -1)
+
+    out = run(ph, amp[0], amp[1])
+    phase = ph @ cpix.T
+    lx, ly = amp[0] @ cpix.T * L, amp[1] @ cpix.T * L
+    with np.errstate(invalid="ignore", over="ignore"):
+        want = np.stack([2 ** lx * np.cos(phase), 2 ** lx * np.sin(phase),
+                         2 ** ly * np.cos(phase), 2 ** ly * np.sin(phase)], 1)
+    want = want.astype(np.float32)
+    nan = np.isnan(want)
+    want[:, 0::2][nan[:, 0::2]] = 1.0
+    want[:, 1::2][nan[:, 1::2]] = 0.0
+    assert np.all(out[35, 0] == 1.0) and np.all(out[35, 1] == 0.0)
+    assert np.all(out[50] == np.array([1, 0, 1, 0], np.float32)[:, None])
+    lmax = np.nan_to_num(np.maximum(np.abs(lx), np.abs(ly)), nan=0.0)[:, None, :]
+    tol = (2e-6 if fast else 1e-6) + 1.2e-7 * lmax
+    err = np.abs(out - want) / np.maximum(1.0, np.abs(want))
+    assert np.all(err <= tol), err.max()
+    # slots 0..14 in a group with a NaN slot (checked path) == the same slots
+    # in a group of their own, bit for bit
+    p2 = np.concatenate([ph[:15], ph[50:51]])
+    x2 = np.concatenate([amp[0][:15], amp[0][:1]])
+    y2 = np.concatenate([amp[1][:15], amp[1][:1]])
+    got = run(p2, x2, y2)
+    np.testing.assert_array_equal(got[:15].view(np.uint32), out[:15].view(np.uint32))
+
+
+@pytest.mark.gpu
 def test_make_aterm_image_gain_kl(tmp_path, gain):
     """make_aterm_image on a gain solution set (soltab "gain000" -> phase000
     + amplitude000), FITS cube vs the reference's make_matrix output."""
