@@ -94,29 +94,6 @@ __device__ __forceinline__ bool group_rev_safe(const double (&af)[KS], double th
   return __builtin_amdgcn_ballot_w64(!(sum < thr)) == 0;  // NaN: not safe
 }
 
-// Gain screens, fast epilogue: a group whose phases are safe (above) and
-// whose every lane's XX / YY coefficient sums bound |log2 A| below 128 (a lane
-// holds a quarter of a slot's directions: sum |coef| log2(10) < 32 / max
-// |Cpix| = rev_thr 2^-10) has no NaN value -- A = exp2 of a finite float
-// below 2^7 is finite, cos / sin of a finite reduced phase are finite -- so
-// the per-value NaN check of the scrub is skipped there (same bits: there is
-// nothing to scrub).  2 x KS fp64 adds and one ballot per group against 2
-// compares per value (profiles/round3_gain_valu_per_value.json: 25 VALU per
-// value).
-constexpr double kAmpThrOfRevThr = 1.0 / 1024.0;
-
-template <int KS>
-__device__ __forceinline__ bool group_amp_finite(const double (&ax)[KS],
-                                                 const double (&ay)[KS], double thr) {
-  double sx = 0.0, sy = 0.0;
-#pragma unroll
-  for (int kk = 0; kk < KS; ++kk) {
-    sx += fabs(ax[kk]);
-    sy += fabs(ay[kk]);
-  }
-  return __builtin_amdgcn_ballot_w64(!(sx < thr && sy < thr)) == 0;  // NaN: no
-}
-
 __device__ __forceinline__ float rev_fixed(double y) {
   const int lo = (int)(unsigned)__double_as_longlong(y);
   return (float)lo * kTwoM32;
@@ -473,11 +450,6 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
     double rf[KS], rx[GAIN ? KS : 1], ry[GAIN ? KS : 1];
     double af[KS], ax[GAIN ? KS : 1], ay[GAIN ? KS : 1];
     bool safe = false;
-    // gain, fixed-point epilogue: the group's values are all finite
-    // (group_amp_finite)
-    constexpr bool kFinCheck = GAIN && kMagic;
-    const double amp_thr = rev_thr * kAmpThrOfRevThr;
-    bool fin = false;
     // IC: the digit rows and the slot flags, one group ahead (the A-lane
     // feeding group row m holds slot dig_row_slot); unconditional loads of a
     // clamped slot (a load behind a branch is a serial round trip), slots
@@ -513,7 +485,6 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
         load_coef_raw<KS>(ry, coef_yy, s0, S, D, l);
         coef_finish<KS>(ax, rx, s0, S, D, l, sx);
         coef_finish<KS>(ay, ry, s0, S, D, l, sx);
-        if constexpr (kFinCheck) fin = safe && group_amp_finite<KS>(ax, ay, amp_thr);
       }
       // the Cpix fragments too must have landed before the group loop: else
       // the compiler, merging this path with the loop's back edge, waits for
@@ -673,6 +644,7 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
         // lane flag, and the 8 selects per pixel run only when some lane of
         // the wave has a NaN (a wave-uniform branch; same bits either way)
         constexpr bool kScrubValues = GAIN || !FAST;
+        bool bad = false;
         // fast epilogue: this row's reduced arguments (frg, above)
         const float(&fr)[kTiles] = frg[r];
 #pragma unroll
@@ -709,21 +681,16 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
             pv[0][t] = pv[2][t] = cf;
             pv[1][t] = pv[3][t] = sf;
           }
-        }
-        // (a group of finite values has nothing to scrub: group_amp_finite)
-        if (kScrubValues && scrub && !(kFinCheck && fin)) {
-          bool bad = false;
-#pragma unroll
-          for (int t = 0; t < kTiles; ++t)
+          if (kScrubValues)
             bad |= __builtin_isunordered(pv[0][t], pv[1][t]) |
                    __builtin_isunordered(pv[2][t], pv[3][t]);
-          if (__builtin_amdgcn_ballot_w64(bad) != 0) {
+        }
+        if (kScrubValues && scrub && __builtin_amdgcn_ballot_w64(bad) != 0) {
 #pragma unroll
-            for (int t = 0; t < kTiles; ++t)
+          for (int t = 0; t < kTiles; ++t)
 #pragma unroll
-              for (int q = 0; q < 4; ++q)
-                if (isnan(pv[q][t])) pv[q][t] = (q & 1) ? 0.0f : 1.0f;
-          }
+            for (int q = 0; q < 4; ++q)
+              if (isnan(pv[q][t])) pv[q][t] = (q & 1) ? 0.0f : 1.0f;
         }
         if (kBE) {
 #pragma unroll
@@ -799,7 +766,6 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
         if constexpr (GAIN) {
           coef_finish<KS>(ax, rx, s1, S, D, l, sx);
           coef_finish<KS>(ay, ry, s1, S, D, l, sx);
-          if constexpr (kFinCheck) fin = safe && group_amp_finite<KS>(ax, ay, amp_thr);
         }
       }
     }

@@ -202,12 +202,13 @@ def test_gain_eval_vs_reference(gain, fast):
 @pytest.mark.gpu
 @pytest.mark.parametrize("fast", [False, True])
 def test_gain_eval_finite_groups_and_scrub(gain, fast):
-    """The fast epilogue skips the per-value NaN check of a 16-slot group
-    whose coefficient sums prove every value finite (kl_eval_impl.h
-    group_amp_finite): groups below that bound, above it (|log2 A| up to 100,
-    finite), with a NaN amplitude or phase coefficient (scrubbed to 1 / 0),
-    against fp64 numpy; and a group's bits do not depend on which of the two
-    paths it took."""
+    """Gain planes of 16-slot groups in four regimes against fp64 numpy:
+    small amplitudes, |log2 A| up to 100 (finite, large values), a NaN
+    amplitude coefficient (its XX planes scrubbed to 1 / 0) and a NaN phase
+    coefficient (all four planes scrubbed), in a partial last group; and a
+    slot's bits do not depend on the other slots of its group (a NaN slot
+    sends the group's phases down the exact reduction, kl_eval_impl.h
+    kRevMagic)."""
     from ska_sdp_screen_fitting_amd._lib import (SF_EVAL_FAST_SINCOS,
                                                  SF_EVAL_NAN_SCRUB)
     torch, dev = _torch_dev()
