@@ -27,11 +27,15 @@ the closed convex cell" (exact orientation tests on float coordinates).
 scipy 1.7.1 (the reference's era) and 1.15.3 give bit-identical Voronoi
 vertices and ridge order on the fixture at every config cell size.  PARITY
 STATUS: the reference's tessellated path cannot run in this image (needs
-shapely), so label rasters are pinned by the reference test criterion
-(patch pixels, tests/test_fit_screens.py:43-128); the ring convention is a
-restatement not checked against GEOS itself, and the pixels it decides
-(2 / 289 at 0.2 deg ... 22 / 16384 at 0.02602 deg,
-profiles/round3_tess_ring_conventions.txt) stay "parity unpinned".
+shapely).  The config-1 raster (0.2 deg, 17^2) is pinned by the reference's
+own rendering of its ``tessellated_0.fits`` (resources/screens_.png, decoded
+by tests/golden/decode_screens_png.py; tests/test_tess_png_pin.py): all 289
+pixels, including the 2 whose label depends on the ring convention, and
+every other ring start / direction that moves a pixel is contradicted by it.
+At the finer cell sizes (1 / 1156 at 0.1 deg ... 22 / 16384 at 0.02602 deg,
+profiles/round3_tess_ring_conventions.txt) the same convention decides a few
+pixels that no reference output shows: those follow the convention pinned
+at 0.2 deg, not an observed GEOS raster.
 """
 
 import numpy as np

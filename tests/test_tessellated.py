@@ -3,9 +3,11 @@ reference's anchors (CPU), fused gather + Gaussian kernel vs the oracle /
 scipy.ndimage and the reference test criterion end to end (GPU).
 
 Parity status: the reference's own tessellated path needs shapely, absent
-from every interpreter here, so no golden raster exists; labels are pinned by
-the reference test's patch-pixel criterion and the survey probe count (5 of
-289 pixels differ from the nearest-direction map on the fixture).
+from every interpreter here, so no raster was generated from it; the config-1
+raster is pinned at every pixel by the reference's rendering of its own
+``tessellated_0.fits`` (tests/test_tess_png_pin.py), and the finer grids by
+the reference test's patch-pixel criterion plus the ring convention that
+rendering confirms.
 """
 
 import os
