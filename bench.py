@@ -44,8 +44,11 @@ WORKLOADS = {
     # BASELINE.json configs[4] (SKA-Low scale): 64 of its 512 stations per
     # GPU, so --gpus 8 is the whole 512 ant x 4000 t x 64 f x 50 dir array
     "config5": (64, 4000, 64, 50, 512, 0.006505),
+    # launcher / collective rehearsals (tests): 80 stations (rank 0 holds
+    # the first 10 up to N = 8, as the reference-station choice needs), 32^2
+    "tiny": (80, 4, 2, 7, 32, 0.10407),
 }
-STRONG = {"config4"}  # first field = stations of the whole job
+STRONG = {"config4", "tiny"}  # first field = stations of the whole job
 
 
 def parse():
@@ -139,7 +142,108 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="gloo: rehearse N ranks on a 1-GPU box (setup "
                          "collectives on the CPU, ranks share the device)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="initialise the process group and run the setup "
+                         "collectives even at world size 1 (exercises the "
+                         "RCCL path on a one-GPU box)")
+    ap.add_argument("--rehearse-cpu", action="store_true",
+                    help="launcher / gloo rehearsal without a GPU: every rank "
+                         "runs the shard setup and its collectives, no kernels "
+                         "(prints a line with value null)")
+    ap.add_argument("--launch-timeout", type=float, default=3000.0,
+                    help="--gpus N without a launcher: seconds before the "
+                         "self-launched ranks are killed")
+    ap.add_argument("--no-config5-leg", action="store_true",
+                    help="skip the one-step config-5 side leg of the default "
+                         "N = 1 run")
     return ap.parse_args()
+
+
+def log(msg):
+    """Progress on stderr (the JSON line alone goes to stdout)."""
+    print(f"bench[{os.environ.get('RANK', '-')}] {time.strftime('%H:%M:%S')} {msg}",
+          file=sys.stderr, flush=True)
+
+
+# --------------------------------------------------------------------------
+# Self-launch: ``python bench.py --gpus N`` without torchrun starts N ranks
+# itself (one child interpreter per GPU, the torchrun environment), so the
+# command form of the N = 1 run works at every N.  The parent never touches
+# the GPU; it forwards the ranks' output (rank 0 prints the JSON line) and
+# exits non-zero if any rank fails or the job times out.  The reference's
+# counterpart is its worker fan-out over processes, stationscreen.py:1056-1077.
+# --------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, timeout_s):
+    import signal
+    import subprocess
+
+    import tempfile
+
+    port = _free_port()
+    procs, outs = [], []
+    log(f"launching {n} ranks (MASTER 127.0.0.1:{port})")
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", ROLE_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        # a rank's stdout goes to a file: libraries print there too (gloo's
+        # peer messages), and only rank 0's JSON line may reach our stdout
+        outs.append(tempfile.TemporaryFile(mode="w+"))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)]
+                                      + sys.argv[1:], env=env, stdout=outs[-1]))
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        deadline = time.time() + 10
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, deadline - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+
+    def on_signal(signum, _frame):
+        stop()
+        raise SystemExit(128 + signum)
+
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, on_signal)
+    t_end = time.time() + timeout_s
+    failed = None
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if bad:
+            failed = f"rank {bad[0][0]} exited with {bad[0][1]}"
+            break
+        if all(c == 0 for c in codes):
+            break
+        if time.time() > t_end:
+            failed = f"timed out after {timeout_s:.0f} s"
+            break
+        time.sleep(0.2)
+    if failed:
+        log(f"self-launched job failed: {failed}; stopping the other ranks")
+        stop()
+    for r, fh in enumerate(outs):
+        fh.seek(0)
+        for ln in fh.read().splitlines():
+            if r == 0 and not failed and ln.startswith("{"):
+                print(ln, flush=True)
+            elif ln.strip():
+                print(f"[rank {r} stdout] {ln}", file=sys.stderr, flush=True)
+        fh.close()
+    return 1 if failed else 0
 
 
 # --------------------------------------------------------------------------
@@ -449,10 +553,11 @@ def dist_block(args, world, record):
     identity (index, PCI address, UUID, host) and its own numbers (slots,
     mean eval-launch time, wall time of the timed steps), gathered from all
     ranks after the timed region."""
+    import torch.distributed as dist
     from ska_sdp_screen_fitting_amd.distributed import gather_records
     per_rank = gather_records(record)
     devs = args.idents
-    return {"backend": args.dist_backend if world > 1 else "none",
+    return {"backend": args.dist_backend if dist.is_initialized() else "none",
             "world": world, "devices": devs, "per_rank": per_rank,
             "distinct_devices": len({d.get("uuid") or d.get("pci") for d in devs})}
 
@@ -568,6 +673,82 @@ def side_legs(ctx, torch, dev, stream, fit_stream, fit, evaluate, coef, bounds,
     return res
 
 
+def config5_leg(timeout_s=420):
+    """BASELINE.json configs[4] (SKA-Low scale) beside the config-4 line: one
+    timed step (after one warmup step) of the shard one of its 8 GPUs runs --
+    64 of 512 stations x 4000 t x 64 f x 50 dir = 16.4 M slots, KL 512^2,
+    fit + eval, integer-digit contraction, discard + checksum mode
+    (kl_screen.py:411-449) -- in a child ``bench.py --workload config5``
+    (its own device buffers, ~45 GB), with its sampled-slot parity and
+    streamed-checksum checks."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--gpus", "1",
+           "--workload", "config5", "--steps", "1", "--warmup", "1",
+           "--no-cpu-baseline", "--no-fits", "--no-side-legs", "--no-config5-leg"]
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    t0 = time.perf_counter()
+    try:
+        p = subprocess.run(cmd, env=env, capture_output=True, text=True,
+                           timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        return {"error": f"timed out after {timeout_s} s"}
+    wall = time.perf_counter() - t0
+    if p.returncode != 0:
+        return {"error": f"exit {p.returncode}: {p.stderr[-600:]}"}
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    rf, sm = r["roofline"], r["check"]["sampled_slots"]
+    return {
+        "workload": r["config"]["workload"],
+        "value": r["value"], "unit": r["unit"], "steps": r["steps"],
+        "warmup": r["warmup"], "ms_per_step": r["ms_per_step"],
+        "dtype": r["dtype"], "stages_ms": r["stages_ms"],
+        "kernel": rf["kernel"], "launch_ms": rf["launch_ms"],
+        "bytes_per_launch": rf["bytes_per_launch"], "achieved_GBs": rf["achieved"],
+        "frac": rf["frac"], "traffic": rf["traffic"], "mfma": r.get("mfma"),
+        "sampled_slots": sm, "checksums_match": sm.get("checksums_match"),
+        "max_abs_err_vs_fp64": sm["max_abs_err_vs_fp64"], "ok": sm["ok"],
+        "child_wall_s": wall,
+        "what": ("one step of config 5's per-GPU shard in a child process "
+                 "(bench.py --workload config5 --steps 1 --warmup 1)")}
+
+
+def rehearse_cpu(args, dist, world, rank, sol, setup, A, A_total, a0):
+    """--rehearse-cpu: the launcher and the gloo setup collectives without
+    a GPU -- every rank builds its shard and runs setup_shard; the line
+    reports each rank's shard and a digest of the setup it received (equal
+    on every rank).  No kernels run: ``value`` is null."""
+    import hashlib
+    t0 = time.perf_counter()
+    if dist.is_initialized():
+        dist.barrier()
+    h = hashlib.sha256()
+    for a in (np.asarray(setup["piercepoints"]), np.asarray(setup["x"]),
+              np.asarray(setup["y"]), setup["ref_phase"].cpu().numpy()):
+        h.update(np.ascontiguousarray(a, np.float64).tobytes())
+    h.update(str(setup["ref_ant"]).encode())
+    T, F = sol.val.shape[:2]
+    record = {"rank": rank, "ant": [a0, a0 + A], "slots": T * F * A,
+              "setup_sha16": h.hexdigest()[:16], "ref_ant": setup["ref_ant"],
+              "st_order": setup["st_order"]}
+    dist_info = dist_block(args, world, record)
+    if dist.is_initialized():
+        dist.barrier()
+    if rank == 0:
+        line = {"metric": METRIC, "value": None, "unit": "screen-slots/s",
+                "n_gpus": world, "steps": 0, "warmup": 0,
+                "ms_per_step": None, "higher_is_better": True,
+                "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+                "data": "synthetic",
+                "config": {"workload": f"{args.workload}: {A_total} ant, rehearsal",
+                           "parallelism": f"ant-shard x{world}"},
+                "rehearsal": ("cpu: self-launch + gloo setup collectives only, "
+                              "no kernels"),
+                "setup_s": time.perf_counter() - t0, "dist": dist_info}
+        print(json.dumps(line), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
 def tess_steps(args, ctx, torch, dev, dist, world, rank, coll_dev, sol, setup,
                A_total, strong):
     """--screen tess: one step = the tessellated fill (gather of the
@@ -616,7 +797,7 @@ def tess_steps(args, ctx, torch, dev, dist, world, rank, coll_dev, sol, setup,
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize(dev)
     evs = []
@@ -629,12 +810,12 @@ def tess_steps(args, ctx, torch, dev, dist, world, rank, coll_dev, sol, setup,
         e1.record(stream)
         evs.append((e0, e1))
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     local_elapsed = elapsed
     tmax = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
-    if world > 1:
+    if dist.is_initialized():
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     elapsed = tmax.item()
     launch_s = float(np.mean([a.elapsed_time(b) for a, b in evs])) * 1e-3
@@ -704,12 +885,15 @@ def tess_steps(args, ctx, torch, dev, dist, world, rank, coll_dev, sol, setup,
             "dist": dist_info,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: start the ranks here (the parent never touches the GPU)
+        raise SystemExit(launch_ranks(args.gpus, args.launch_timeout))
     import torch
     import torch.distributed as dist
 
@@ -718,23 +902,34 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    n_dev = torch.cuda.device_count()
-    gpu = local_rank if args.dist_backend == "nccl" else local_rank % max(n_dev, 1)
-    torch.cuda.set_device(gpu)
-    dev = torch.device("cuda", gpu)
+    if args.rehearse_cpu and args.dist_backend != "gloo":
+        raise SystemExit("--rehearse-cpu needs --dist-backend gloo")
+    if args.rehearse_cpu:
+        gpu, dev = None, torch.device("cpu")
+    else:
+        n_dev = torch.cuda.device_count()
+        gpu = local_rank if args.dist_backend == "nccl" else local_rank % max(n_dev, 1)
+        torch.cuda.set_device(gpu)
+        dev = torch.device("cuda", gpu)
     coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
-    if world > 1:
+    if world > 1 or args.force_dist:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
+    log(f"rank {rank}/{world} backend "
+        f"{args.dist_backend if dist.is_initialized() else 'none'} device {dev}")
     # which physical GPU every rank drives, gathered once before any work:
     # under nccl two ranks on one card end the job here
     from ska_sdp_screen_fitting_amd.distributed import (check_distinct_devices,
                                                         device_identity,
                                                         gather_records)
-    ident = dict(device_identity(torch, dev), rank=rank, local_rank=local_rank,
-                 host=socket.gethostname())
+    if args.rehearse_cpu:
+        ident = {"index": None, "pci": f"cpu:{socket.gethostname()}:{os.getpid()}",
+                 "uuid": "", "name": "cpu (rehearsal)"}
+    else:
+        ident = device_identity(torch, dev)
+    ident = dict(ident, rank=rank, local_rank=local_rank, host=socket.gethostname())
     idents = gather_records(ident)
     try:
         check_distinct_devices(idents, args.dist_backend if world > 1 else "none")
@@ -772,8 +967,11 @@ def main():
                          ant_offset=a0, n_ant_total=A_total)
     setup = setup_shard(sol, a0, A_total, FIELD_RA_DEG, FIELD_DEC_DEG,
                         FIELD_WIDTH_DEG, cell,
-                        device=coll_dev if world > 1 else "cpu")
+                        device=coll_dev if dist.is_initialized() else "cpu")
     assert len(setup["x"]) == N
+    log(f"shard ready: ant [{a0}, {a0 + A}) of {A_total}, {T * F * A} slots")
+    if args.rehearse_cpu:
+        return rehearse_cpu(args, dist, world, rank, sol, setup, A, A_total, a0)
 
     ctx = get_context(gpu)
     if args.screen == "tess":
@@ -946,16 +1144,18 @@ def main():
     if args.eval_only:
         for c in range(n_chunks):
             fit(c, first_fit_stream)
+    log(f"warmup: {args.warmup} steps")
     run_steps(args.warmup)
     torch.cuda.synchronize(dev)
 
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize(dev)
+    log(f"timed: {args.steps} steps")
     t0 = time.perf_counter()
     ev = run_steps(args.steps)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     local_elapsed = elapsed
@@ -967,7 +1167,7 @@ def main():
     t_eval = float(np.sum(eval_launch)) * 1e-3 / args.steps
     t_eval_launch = float(np.mean(eval_launch)) * 1e-3
     tmax = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
-    if world > 1:
+    if dist.is_initialized():
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     elapsed = tmax.item()
 
@@ -996,8 +1196,14 @@ def main():
 
     side = {}
     if not args.no_side_legs and not args.eval_only:
+        log("side legs")
         side = side_legs(ctx, torch, dev, stream, first_fit_stream, fit, evaluate,
                          coef, bounds, F, A, D, P, out, ring, flags, gain, amp)
+    if (rank == 0 and world == 1 and args.workload == "config4" and not gain
+            and not args.no_config5_leg and not args.as_shard_of
+            and not args.eval_only):
+        log("config-5 leg (child process)")
+        side["config5"] = config5_leg()
 
     if rank == 0:
         # SURVEY.md §8(d), per step; gain screens read three coefficient sets
@@ -1094,8 +1300,10 @@ def main():
                                 for k, v in (fe or {}).get("kernels", {}).items()},
             }
         if not args.no_fits and world == 1:
+            log("FITS wall-clock legs")
             line["fits_wallclock"] = fits_wallclock(config3=not args.no_fits_config3)
         if not args.no_cpu_baseline and world == 1:
+            log("CPU baseline")
             nw, rule = cpu_share()
             if args.cpu_workers:
                 nw, rule = args.cpu_workers, "--cpu-workers"
@@ -1116,7 +1324,7 @@ def main():
     for h in (masked_handle, fit_handle):
         if h is not None:
             ctx.stream_destroy(h)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

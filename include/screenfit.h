@@ -174,8 +174,10 @@ int sf_device_cus(sf_ctx* ctx, int* n_cu);
  * turns -- for phase screens with D >= 45, on the fast (hardware sincos)
  * epilogue with float4-aligned output (gain screens keep fp64); slots whose
  * coefficients are not finite or out of the digit range take the fp64
- * contraction.  |error| <= 2^-28 turn of phase (2^-32 typical), below the
- * fp32 rounding of the reduced phase; it runs in the register tile and the
+ * contraction.  |error| < 2^-27 turn of phase over the allowed ranges
+ * (7.06e-9 turn at D = 60, |coef / 2 pi| = 8.03 turns, |Cpix| = 1905 with
+ * every rounding aligned; ~2^-32 at the BASELINE configs), below the fp32
+ * rounding of the reduced phase (up to 2^-26 turn); it runs in the register tile and the
  * LDS-staged kernels alike (same bits), SF_EVAL_KERNEL_SHB is replaced by the
  * register tile (sf_get_eval_kernel / sf_get_eval_contraction say so). */
 #define SF_OPT_EVAL_INT 15

@@ -94,6 +94,7 @@ int sf_destroy(sf_ctx* ctx) {
   hipFree(ctx->d_cdig);
   hipFree(ctx->d_kdig);
   hipFree(ctx->d_kflag);
+  if (ctx->kdig_read) (void)hipEventDestroy(ctx->kdig_read);
   hipFree(ctx->d_skip);
   hipFree(ctx->d_st_order);
   hipFree(ctx->d_keys);
@@ -406,6 +407,10 @@ int sf_set_grid(sf_ctx* ctx, const double* x, int nx, const double* y,
                 int ny) {
   SF_REQUIRE(ctx && ctx->D > 0, SF_EINVAL, "sf_set_grid: call sf_set_basis first");
   SF_REQUIRE(x && y && nx >= 1 && ny >= 1, SF_EINVAL, "sf_set_grid: bad grid");
+  for (int i = 0; i < nx; ++i)
+    SF_REQUIRE(std::isfinite(x[i]), SF_EINVAL, "sf_set_grid: non-finite x coordinate");
+  for (int j = 0; j < ny; ++j)
+    SF_REQUIRE(std::isfinite(y[j]), SF_EINVAL, "sf_set_grid: non-finite y coordinate");
   SF_REQUIRE((int64_t)nx * ny <= ((int64_t)1 << 31), SF_EINVAL,
              "sf_set_grid: grid too large");
   SF_HIP(hipSetDevice(ctx->device));
@@ -435,28 +440,43 @@ int sf_set_grid(sf_ctx* ctx, const double* x, int nx, const double* y,
   } else {
     rc = sf::launch_cpix(ctx, dx, dy);
   }
-  // largest |Cpix| over the grid (kl_cpix_kernel's formula on the farthest
-  // corner of each direction, 1 % margin for the device pow): the
-  // fixed-point phase epilogue's group bound and the integer contraction's
-  // range check
+  // largest |Cpix| over the grid: |Cpix| = (d^2 / r0^2)^(beta / 2) / 2 is
+  // monotonic in the distance, so its maximum is at the farthest grid point
+  // of each direction (beta > 0) or at the nearest one (beta < 0); both are
+  // taken, with 1 % margin for the device pow.  The fixed-point phase
+  // epilogue's group bound and the integer contraction's range check.  A
+  // non-finite value (beta < 0 on a piercepoint) disables both.
   double cmax = 0.0;
   for (int d = 0; d < ctx->D; ++d) {
-    double mx = 0.0, my = 0.0;
-    for (int i = 0; i < nx; ++i) mx = std::fmax(mx, std::fabs(ctx->h_pp[3 * d] - x[i]));
-    for (int j = 0; j < ny; ++j) my = std::fmax(my, std::fabs(ctx->h_pp[3 * d + 1] - y[j]));
+    const double px = ctx->h_pp[3 * d], py = ctx->h_pp[3 * d + 1];
+    double mx = 0.0, my = 0.0, nxd = HUGE_VAL, nyd = HUGE_VAL;
+    for (int i = 0; i < nx; ++i) {
+      mx = std::fmax(mx, std::fabs(px - x[i]));
+      nxd = std::fmin(nxd, std::fabs(px - x[i]));
+    }
+    for (int j = 0; j < ny; ++j) {
+      my = std::fmax(my, std::fabs(py - y[j]));
+      nyd = std::fmin(nyd, std::fabs(py - y[j]));
+    }
     const double z = ctx->h_pp[3 * d + 2];
-    const double d2 = mx * mx + my * my + z * z;
-    cmax = std::fmax(cmax, 1.01 * 0.5 * std::pow(d2 / (ctx->r0 * ctx->r0), ctx->beta / 2.0));
+    for (const double d2 : {mx * mx + my * my + z * z, nxd * nxd + nyd * nyd + z * z}) {
+      const double c = 1.01 * 0.5 * std::pow(d2 / (ctx->r0 * ctx->r0), ctx->beta / 2.0);
+      cmax = std::isfinite(c) ? std::fmax(cmax, c) : HUGE_VAL;
+    }
   }
   // the integer-digit contraction (D >= 45): rint(Cpix * 2^36) must fit 6
-  // balanced base-256 digits (|.| < 2^46.99); 2^46.9 leaves the margin
+  // balanced base-256 digits (|.| < 2^46.99); 2^46.9 leaves the margin, and
+  // kl_cdig_kernel reports any value that still does not fit
   ctx->dig_ok = 0;
+  int* dbad = nullptr;
   if (rc == SF_OK && ctx->ksteps >= 12 && std::isfinite(cmax) &&
       cmax * 68719476736.0 < std::ldexp(1.0, 46) * 1.86) {
     // (no memory for the digits: the fp64 contraction serves, not an error)
     if (dev_alloc(&ctx->d_cdig, (size_t)ctx->n_pix_blocks * sf::kEvalWaves *
-                                    sf::kDigits * sf::kTiles * 64 * 16) == SF_OK) {
-      rc = sf::launch_cdig(ctx, dx, dy);
+                                    sf::kDigits * sf::kTiles * 64 * 16) == SF_OK &&
+        dev_alloc(&dbad, 1) == SF_OK &&
+        hipMemsetAsync(dbad, 0, sizeof(int), ctx->stream) == hipSuccess) {
+      rc = sf::launch_cdig(ctx, dx, dy, dbad);
       if (rc == SF_OK) ctx->dig_ok = 1;
     }
   }
@@ -464,6 +484,12 @@ int sf_set_grid(sf_ctx* ctx, const double* x, int nx, const double* y,
     set_error("sf_set_grid: pixel basis kernel failed");
     rc = SF_EIO;
   }
+  if (ctx->dig_ok) {
+    int bad = 1;
+    if (hipMemcpy(&bad, dbad, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess || bad)
+      ctx->dig_ok = 0;
+  }
+  (void)hipFree(dbad);
   (void)hipFree(dx);
   (void)hipFree(dy);
   if (rc == SF_OK) {
@@ -539,6 +565,9 @@ static int upload_gaussian(sf_ctx* ctx, double sigma, int* R_out) {
   // read the previous ones, and the host vector dies here -- drain the
   // device, copy on the context's stream, wait for the copy
   SF_HIP(hipDeviceSynchronize());
+  // until the copy below has landed d_gw holds no sigma's weights: a failure
+  // on the way must not leave the cache naming the old sigma
+  ctx->gw_sigma = -1.0;
   if (ctx->gw_cap < w.size()) {
     if (ctx->d_gw) (void)hipFree(ctx->d_gw);
     ctx->d_gw = nullptr;

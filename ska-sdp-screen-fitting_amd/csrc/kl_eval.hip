@@ -89,10 +89,13 @@ int launch_cpix(sf_ctx* ctx, const double* d_x, const double* d_y) {
 // direction d = 16 (l >> 4) + jb of pixel column l & 15 of tile t, i.e. digit
 // i of rint(Cpix[p][d] * 2^36) (0 past D or the grid).  Cpix is
 // kl_cpix_kernel's value bit for bit (pix_cov).
+// A value that is not finite or does not fit the 6 digits (the host's range
+// check is a bound, not a proof) sets *bad, and sf_set_grid keeps the fp64
+// contraction for the grid.
 __global__ __launch_bounds__(256) void kl_cdig_kernel(
     const double* __restrict__ pp, int D, double r0, double beta,
     const double* __restrict__ xs, int nx, const double* __restrict__ ys,
-    int ny, int64_t n_frag, v4i* __restrict__ cdig) {
+    int ny, int64_t n_frag, v4i* __restrict__ cdig, int* __restrict__ bad) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n_frag) return;
   const int l = (int)(e & 63);
@@ -113,8 +116,11 @@ __global__ __launch_bounds__(256) void kl_cdig_kernel(
       const int ix = (int)(p % nx), iy = (int)(p / nx);
       const double c = pix_cov(pp[3 * d], pp[3 * d + 1], pp[3 * d + 2], xs[ix], ys[iy],
                                r0 * r0, beta / 2.0);
+      const double y = ldexp(c, kSigma);
+      const bool fin = __builtin_isfinite(y) && fabs(y) < 4.6e18;  // llrint range
       int8_t dg[kDigits];
-      (void)dig_split((long long)rint(ldexp(c, kSigma)), dg);  // fits: sf_set_grid
+      const long long rem = dig_split(fin ? (long long)rint(y) : 0ll, dg);
+      if (!fin || rem != 0) atomicOr(bad, 1);
       val = dg[i];
     }
     u.b[jb] = val;
@@ -122,13 +128,14 @@ __global__ __launch_bounds__(256) void kl_cdig_kernel(
   cdig[e] = u.v;
 }
 
-int launch_cdig(sf_ctx* ctx, const double* d_x, const double* d_y) {
+int launch_cdig(sf_ctx* ctx, const double* d_x, const double* d_y, int* d_bad) {
   const int64_t n_wpb = ctx->n_pix_blocks * kEvalWaves;
   const int64_t n = n_wpb * kDigits * kTiles * 64;
   const int64_t blocks = (n + 255) / 256;
   hipLaunchKernelGGL(kl_cdig_kernel, dim3((unsigned)blocks), dim3(256), 0,
                      ctx->stream, ctx->d_pp, ctx->D, ctx->r0, ctx->beta, d_x,
-                     ctx->nx, d_y, ctx->ny, n, reinterpret_cast<v4i*>(ctx->d_cdig));
+                     ctx->nx, d_y, ctx->ny, n, reinterpret_cast<v4i*>(ctx->d_cdig),
+                     d_bad);
   SF_HIP(hipGetLastError());
   return SF_OK;
 }

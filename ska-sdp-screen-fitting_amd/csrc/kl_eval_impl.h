@@ -1221,6 +1221,7 @@ constexpr int64_t kDigChunk = (int64_t)1 << 20;
 
 inline int ensure_kdig(sf_ctx* ctx, int64_t slots) {
   if (ctx->kdig_slots >= slots) return SF_OK;
+  // (hipFree waits for the device, so no reader of the old buffers remains)
   (void)hipFree(ctx->d_kdig);
   (void)hipFree(ctx->d_kflag);
   ctx->d_kdig = nullptr;
@@ -1236,11 +1237,24 @@ inline int ensure_kdig(sf_ctx* ctx, int64_t slots) {
 }
 
 // Prepass of one integer-contraction launch: the digit rows and flags of S
-// slots
+// slots.  The buffers are the context's, so a launch on another stream may
+// still be reading them: the prepass waits for the last reader first
+// (kdig_read, recorded by kdig_done after every integer launch; on the same
+// stream the wait is already satisfied by stream order).
 inline int run_kdig(sf_ctx* ctx, const double* cb, int64_t S) {
+  if (!ctx->kdig_read)
+    SF_HIP(hipEventCreateWithFlags(&ctx->kdig_read, hipEventDisableTiming));
+  else
+    SF_HIP(hipStreamWaitEvent(ctx->stream, ctx->kdig_read, 0));
   hipLaunchKernelGGL(kl_kdig_kernel<0>, dim3((unsigned)((S + 3) / 4)), dim3(256), 0,
                      ctx->stream, cb, ctx->D, S, kInv2Pi, ctx->d_kdig, ctx->d_kflag);
   SF_HIP(hipGetLastError());
+  return SF_OK;
+}
+
+// after the launch that read the digits run_kdig wrote
+inline int kdig_done(sf_ctx* ctx) {
+  SF_HIP(hipEventRecord(ctx->kdig_read, ctx->stream));
   return SF_OK;
 }
 
@@ -1316,6 +1330,10 @@ int launch_eval_lds(sf_ctx* ctx, const double* coef, int64_t S_all,
   }
 #undef SF_LAUNCH_LDS
   SF_HIP(hipGetLastError());
+  if (ic) {
+    const int rc = kdig_done(ctx);
+    if (rc != SF_OK) return rc;
+  }
   }
   return SF_OK;
 }
@@ -1373,6 +1391,10 @@ int launch_eval_int(sf_ctx* ctx, const double* coef, int64_t S_all, float* out,
     }
 #undef SF_LAUNCH_IC
     SF_HIP(hipGetLastError());
+    {
+      const int rc = kdig_done(ctx);
+      if (rc != SF_OK) return rc;
+    }
   }
   return SF_OK;
 }

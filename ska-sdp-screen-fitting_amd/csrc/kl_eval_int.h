@@ -13,7 +13,8 @@
 //   * Cq = rint(Cpix * 2^36) and cq = rint(coef / 2 pi * 2^44) are split into
 //     6 balanced base-256 digits each (Cq = sum_i a_i 256^i, a_i in
 //     [-128, 127]); the grid must have |Cpix| < 2^10.9 (sf_set_grid checks),
-//     a slot |coef / 2 pi| < ~7.9 turns (the prepass checks, per slot);
+//     a slot -8.031 <= coef / 2 pi <= 7.969 turns (the digit range: the
+//     prepass checks, per slot);
 //   * sum_d Cq cq 2^-80 turn = sum_{i,j} P_ij 2^(8 (i + j) - 80) with
 //     P_ij = sum_d a_i[d] b_j[d] over the D <= 64 directions of one MFMA's
 //     K, exact in int32 (|P| < 2^23);
@@ -24,10 +25,13 @@
 //     quantity the fixed-point fp64 epilogue reads off its accumulator
 //     (kl_eval_impl.h kRevMagic), at half the MFMA cycles of the 13 fp64
 //     k-steps of D = 50;
-//   * error: Cq rounding sum |coef| 2^-37, cq rounding sum |Cpix| 2^-45, the
-//     dropped diagonals and the shifts of the combine ~1.3 units: <= 2^-28
-//     turn over the allowed ranges, ~2^-32 at the BASELINE configs (fp32
-//     rounding of the reduced phase: up to 2^-26).
+//   * error (turns): Cq rounding sum |coef / 2 pi| 2^-37 (<= 3.51e-9 at
+//     D = 60 x 8.031 turns), cq rounding sum |Cpix| 2^-45 (<= 3.25e-9 at
+//     60 x 1904.6), the dropped diagonals and the shifts of the combine
+//     <= 1.3 units (3.0e-10): < 7.06e-9 < 2^-27 turn over the allowed
+//     ranges (an adversarial case with every rounding aligned reaches
+//     6.2e-9, tests/test_int_digits.py), ~2^-32 at the BASELINE configs;
+//     the fp32 rounding of the reduced phase is up to 2^-26.
 //
 // Used for phase screens from D = 45 (the register tile's range), fast
 // epilogue: below, the LDS-staged fp64 kernels are store-bound already.  Gain

@@ -73,6 +73,9 @@ struct sf_ctx {
   int8_t* d_kdig = nullptr;    // [slot][6][64]
   uint8_t* d_kflag = nullptr;  // [slot]: 1 = integer path
   int64_t kdig_slots = 0;      // slots the buffers hold
+  // recorded after every launch that reads d_kdig / d_kflag: the next
+  // prepass (on whatever stream) waits for it before rewriting them
+  hipEvent_t kdig_read = nullptr;
   double h_pp[3 * SF_MAX_DIR] = {};  // host copy of the piercepoints
   // fit scratch
   uint8_t* d_skip = nullptr;   // [F][A] block skip flags
@@ -153,7 +156,7 @@ int launch_fit_general(sf_ctx* ctx, const int* slot_list, const int* n_list,
                        double* resid, float* w_out, int32_t* order_out);
 int launch_basis(sf_ctx* ctx);
 int launch_cpix(sf_ctx* ctx, const double* d_x, const double* d_y);
-int launch_cdig(sf_ctx* ctx, const double* d_x, const double* d_y);
+int launch_cdig(sf_ctx* ctx, const double* d_x, const double* d_y, int* d_bad);
 int launch_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,
                int F, int A, const sf_fit_params* p, double* coef,
                double* resid, float* w_out, int32_t* order_out);

@@ -340,15 +340,19 @@ class Context:
         ring = max(int(S if ring_slots is None else ring_slots), 1)
         n = int(S) * int(D)
         if hasattr(labels, "min") and labels.numel():
-            # validated once per label tensor (its storage, size, in-place
-            # version and D): every chunk of a Screen.write passes the same
-            # template, and min / max are two reductions + two host syncs
-            key = (labels.data_ptr(), labels.numel(), labels._version, int(D))
-            if key != getattr(self, "_labels_ok", None):
+            # validated once per label tensor OBJECT (held by a weak
+            # reference, so a new tensor in the freed storage of the old one
+            # is validated again), its in-place version and D: every chunk of
+            # a Screen.write passes the same template, and min / max are two
+            # reductions + two host syncs
+            import weakref
+            prev = getattr(self, "_labels_ok", None)
+            key = (labels._version, int(D))
+            if prev is None or prev[0]() is not labels or prev[1] != key:
                 lo, hi = int(labels.min()), int(labels.max())
                 if lo < 1 or hi > int(D):
                     raise ValueError(f"labels: values {lo}..{hi} outside 1..{D}")
-                self._labels_ok = key
+                self._labels_ok = (weakref.ref(labels), key)
         _check(self.lib.sf_tess_fill(
             self.h, self._dev(labels, np.int32, int(nx) * int(ny), "labels"),
             int(nx), int(ny), self._dev(phase, np.float64, n, "phase"),

@@ -45,8 +45,10 @@ def setup_shard(local, ant_offset, n_ant_total, rad, dec, width_deg,
     import torch
     import torch.distributed as dist
 
-    rank = dist.get_rank(group) if dist.is_initialized() else 0
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    # collectives run whenever a process group exists (at world size 1 too,
+    # so a one-GPU job can exercise the RCCL path)
+    coll = dist.is_initialized()
+    rank = dist.get_rank(group) if coll else 0
     T, F, A, D = local.val.shape
     if order is None:
         order = min(20, D - 1)
@@ -71,7 +73,7 @@ def setup_shard(local, ant_offset, n_ant_total, rad, dec, width_deg,
         hdr[8 + 3 * D:8 + 3 * D + n_grid] = torch.from_numpy(x)
         hdr[8 + 3 * D + n_grid:] = torch.from_numpy(y)
     hdr = hdr.to(device)
-    if world > 1:
+    if coll:
         dist.broadcast(hdr, 0, group=group)
     hdr = hdr.cpu().numpy()
     ref = int(hdr[0])
@@ -85,7 +87,7 @@ def setup_shard(local, ant_offset, n_ant_total, rad, dec, width_deg,
     dd = pos - refpos
     dloc = np.sqrt(dd[:, 0] ** 2 + dd[:, 1] ** 2 + dd[:, 2] ** 2)
     dmax = torch.tensor([float(dloc.max())], dtype=torch.float64, device=device)
-    if world > 1:
+    if coll:
         dist.all_reduce(dmax, op=dist.ReduceOp.MAX, group=group)
     scale = np.float32(dmax.item())
     root = np.sqrt((dloc / scale).astype(np.float32))
@@ -96,7 +98,7 @@ def setup_shard(local, ant_offset, n_ant_total, rad, dec, width_deg,
     if rank == 0:
         refph = torch.from_numpy(np.ascontiguousarray(local.val[:, :, ref, :]))
     refph = refph.to(device)
-    if world > 1:
+    if coll:
         dist.broadcast(refph, 0, group=group)
     return dict(ref_ant=ref, st_order=st_order, piercepoints=pp,
                 mid_ra=float(hdr[4]), mid_dec=float(hdr[5]), x=x, y=y,
@@ -118,7 +120,7 @@ def gather_records(record, group=None):
     """Every rank's ``record`` (a JSON-able dict), in rank order, on every
     rank (all_gather_object; one call, outside any timed region)."""
     import torch.distributed as dist
-    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+    if not dist.is_initialized():
         return [record]
     out = [None] * dist.get_world_size(group)
     dist.all_gather_object(out, record, group=group)

@@ -201,16 +201,21 @@ class KLScreen(Screen):
 
     def make_matrix(self, t_start_index, t_stop_index, freq_ind, stat_ind,
                     cellsize_deg, out_dir, ncpu):
-        """(t_stop - t_start, 4, ny, nx) float64 (kl_screen.py:192-380); the
-        values carry the float32 rounding of the FITS cube (Q12)."""
+        """(t_stop - t_start, 4, ny, nx) float64 (kl_screen.py:192-380): the
+        raw cos / sin (x 10 ** amplitude) planes, NaN where a coefficient is
+        NaN -- the reference scrubs NaNs only in ``Screen.write``, after the
+        optional smoothing (screen.py:353-378), and so does ``write_chunk``.
+        The values carry the float32 rounding of the FITS cube (Q12)."""
         del out_dir, ncpu
         sl = np.s_[t_start_index:t_stop_index, freq_ind, stat_ind, :]
         coef = np.asarray(self.vals_ph)[sl]
         ev = self.evaluator(cellsize_deg)
+        flags = DEFAULT_FLAGS & ~SF_EVAL_NAN_SCRUB
         if self.phase_only:
-            return ev.eval_host(coef).astype(np.float64)
+            return ev.eval_host(coef, flags=flags).astype(np.float64)
         amp = np.asarray(self.vals_amp)[sl]
-        return ev.eval_host(coef, amp[..., 0], amp[..., 1]).astype(np.float64)
+        return ev.eval_host(coef, amp[..., 0], amp[..., 1],
+                            flags=flags).astype(np.float64)
 
     def write_chunk(self, writer, g_start, g_stop, cellsize_deg, smooth_pix,
                     max_batch_bytes=1 << 30):

@@ -289,7 +289,8 @@ class VoronoiScreen(Screen):
         a = np.ascontiguousarray(a, np.float64)
         return torch.from_numpy(a.reshape(-1, a.shape[-1])).to(dev)
 
-    def eval_host(self, phase, smooth_pix=0.0, amp_xx=None, amp_yy=None):
+    def eval_host(self, phase, smooth_pix=0.0, amp_xx=None, amp_yy=None,
+                  flags=SF_EVAL_NAN_SCRUB):
         """[..., D] referenced phases (optional amplitudes) -> float32
         [..., 4, ny, nx] (gather + optional Gaussian smoothing) on the GPU."""
         import torch
@@ -300,22 +301,24 @@ class VoronoiScreen(Screen):
         axx = None if amp_xx is None else self._upload(amp_xx)
         ayy = None if amp_yy is None else self._upload(amp_yy)
         out = torch.empty((ph.shape[0], 4, ny, nx), dtype=torch.float32, device=dev)
-        self.eval_device(ph, out, smooth_pix, amp_xx=axx, amp_yy=ayy)
+        self.eval_device(ph, out, smooth_pix, flags, amp_xx=axx, amp_yy=ayy)
         return out.cpu().numpy().reshape(lead + (4, ny, nx))
 
     def make_matrix(self, t_start_index, t_stop_index, freq_ind, stat_ind,
                     cellsize_deg, out_dir, ncpu):
-        """(t_stop - t_start, 4, ny, nx) (voronoi_screen.py:132-216)."""
+        """(t_stop - t_start, 4, ny, nx) float64 (voronoi_screen.py:132-216):
+        the gathered (amplitude x) cos / sin, NaN where a phase is NaN; the
+        NaN scrub belongs to ``Screen.write`` (screen.py:364-378)."""
         del ncpu
         if self.data_rasertize_template is None:
             self.make_rasertize_template(cellsize_deg, out_dir)
         sl = np.s_[t_start_index:t_stop_index, freq_ind, stat_ind, :]
         ph = self.vals_ph[sl]
         if self.phase_only:
-            return self.eval_host(ph).astype(np.float64)
+            return self.eval_host(ph, flags=0).astype(np.float64)
         amp = np.asarray(self.vals_amp)[sl]
-        return self.eval_host(ph, amp_xx=amp[..., 0],
-                              amp_yy=amp[..., 1]).astype(np.float64)
+        return self.eval_host(ph, amp_xx=amp[..., 0], amp_yy=amp[..., 1],
+                              flags=0).astype(np.float64)
 
     def write(self, out_dir, cellsize_deg, smooth_pix=0, ncpu=0):
         if self.data_rasertize_template is None:

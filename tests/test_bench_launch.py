@@ -1,0 +1,85 @@
+"""``bench.py --gpus N`` without a launcher starts its own N ranks (CPU).
+
+The driver runs ``python bench.py --gpus N`` at N = 1 and, for the scaling
+curve, N = 2 / 4 / 8; torchrun sets WORLD_SIZE for the ranks, a bare command
+does not.  bench.py then spawns N child interpreters with the torchrun
+environment (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT),
+forwards rank 0's JSON line and fails when any rank fails.  These tests run
+the launcher with ``--rehearse-cpu`` (gloo, the shard setup and its
+collectives, no kernels) on the tiny workload: the reference's counterpart is
+its worker fan-out, stationscreen.py:1056-1077.
+"""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run_bench(*extra, timeout=240):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(OMP_NUM_THREADS="1")
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *extra],
+                          cwd=REPO, env=env, capture_output=True, text=True,
+                          timeout=timeout)
+
+
+def one_line(p):
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_self_launch_ranks(n):
+    p = run_bench("--gpus", str(n), "--dist-backend", "gloo", "--workload", "tiny",
+                  "--rehearse-cpu")
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = one_line(p)
+    d = line["dist"]
+    assert line["n_gpus"] == n and d["world"] == n and d["backend"] == "gloo"
+    assert len(d["per_rank"]) == n and len(d["devices"]) == n
+    assert [r["rank"] for r in d["per_rank"]] == list(range(n))
+    # contiguous antenna shards covering the 80-station array
+    spans = [tuple(r["ant"]) for r in d["per_rank"]]
+    assert spans[0][0] == 0 and spans[-1][1] == 80
+    assert all(spans[k][1] == spans[k + 1][0] for k in range(n - 1))
+    # every rank received the same broadcast setup ...
+    assert len({r["setup_sha16"] for r in d["per_rank"]}) == 1
+    # ... and the same station orders as the unsharded run (max over ranks)
+    one = one_line(run_bench("--gpus", "1", "--dist-backend", "gloo", "--workload",
+                             "tiny", "--rehearse-cpu"))
+    whole = one["dist"]["per_rank"][0]
+    assert sum((r["st_order"] for r in d["per_rank"]), []) == whole["st_order"]
+    assert d["per_rank"][0]["setup_sha16"] == whole["setup_sha16"]
+
+
+def test_self_launch_fails_when_a_rank_fails():
+    """A rank that exits non-zero (here every rank refuses --rehearse-cpu
+    under nccl) makes the launcher exit non-zero with no JSON line."""
+    p = run_bench("--gpus", "2", "--dist-backend", "nccl", "--workload", "tiny",
+                  "--rehearse-cpu")
+    assert p.returncode != 0
+    assert p.stdout.strip() == ""
+    assert "self-launched job failed" in p.stderr
+
+
+def test_self_launch_timeout_kills_ranks():
+    p = run_bench("--gpus", "2", "--dist-backend", "gloo", "--workload", "tiny",
+                  "--rehearse-cpu", "--launch-timeout", "0.05", timeout=60)
+    assert p.returncode != 0
+    assert "timed out" in p.stderr
+
+
+def test_world_size_mismatch_still_refused():
+    """Under a launcher (WORLD_SIZE set) --gpus must match it."""
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2",
+                        "--rehearse-cpu", "--dist-backend", "gloo"],
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0 and "WORLD_SIZE=1" in p.stderr

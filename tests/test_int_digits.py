@@ -11,8 +11,10 @@ compares R 2^-32 with:
     diagonals k <= 3 and the two arithmetic shifts separate them:
     <= ~1.3 units of 2^-32 turn);
   * the fp64 phase sum_d Cpix coef / 2 pi (adds the operand rounding:
-    sum |coef / 2 pi| 2^-37 + sum |Cpix| 2^-45, <= 2^-28 turn over the
-    allowed ranges).
+    sum |coef / 2 pi| 2^-37 + sum |Cpix| 2^-45; over the allowed ranges --
+    D <= 60, |coef / 2 pi| <= 8.031 turns (the digit range), |Cpix| < 1904.6
+    (sf_set_grid) -- at most 3.51e-9 + 3.25e-9 + 0.30e-9 = 7.06e-9 turn
+    < 2^-27, which the adversarial case below approaches).
 CPU only (no GPU): pins the algorithm the GPU tests exercise through cos/sin.
 """
 
@@ -49,10 +51,19 @@ def combine(p):
 
 def int_phase(cpix_row, coef):
     """R (units of 2^-32 turn, in [-2^31, 2^31)) for one (slot, pixel)"""
-    a = [digits(int(np.rint(np.ldexp(c, SIGMA))))[0] for c in cpix_row]
+    return int_phase_turns(cpix_row, [x / (2 * np.pi) for x in coef])
+
+
+def int_phase_turns(cpix_row, turns):
+    """int_phase with the coefficients already in turns (coef / 2 pi)"""
+    a = []
+    for c in cpix_row:
+        dg, rem = digits(int(np.rint(np.ldexp(c, SIGMA))))
+        assert rem == 0, "Cpix out of the digit range"
+        a.append(dg)
     b = []
-    for x in coef:
-        dg, rem = digits(int(np.rint(np.ldexp(x / (2 * np.pi), TAU))))
+    for x in turns:
+        dg, rem = digits(int(np.rint(np.ldexp(x, TAU))))
         assert rem == 0, "coefficient out of the digit range"
         b.append(dg)
     p = []
@@ -61,7 +72,7 @@ def int_phase(cpix_row, coef):
         for i in range(NDIG):
             j = k - i
             if 0 <= j < NDIG:
-                s += sum(a[d][i] * b[d][j] for d in range(len(coef)))
+                s += sum(a[d][i] * b[d][j] for d in range(len(turns)))
         assert abs(s) < 2 ** 31  # exact in int32 (the MFMA accumulators)
         p.append(wrap32(s))
     return combine(p)
@@ -113,3 +124,50 @@ def test_digit_split_range():
         assert all(-128 <= d <= 127 for d in dg)
     for v in (127 * m + 1, -128 * m - 1, 2 ** 47):
         assert digits(v)[1] != 0
+
+
+# the allowed ranges (kl_eval_int.h): D <= SF_MAX_DIR = 60; coefficients
+# whose rint(coef / 2 pi 2^44) fits 6 balanced digits ([-128 m, 127 m],
+# m = (256^6 - 1) / 255: -8.031 .. 7.969 turns); |Cpix| 2^36 < 1.86 2^46
+# (sf_set_grid's cmax check, which carries a 1 % margin itself)
+M6 = (256 ** 6 - 1) // 255
+K_POS, K_NEG = 127 * M6 / 2.0 ** TAU, -128 * M6 / 2.0 ** TAU
+CPIX_MAX = 1.86 * 2.0 ** 10
+BOUND_TURNS = 2.0 ** -27   # kl_eval_int.h / include/screenfit.h
+
+
+def test_stated_bound_covers_the_range_limits():
+    """The per-term accounting at the range limits stays below 2^-27."""
+    worst = (60 * max(K_POS, -K_NEG) * 2.0 ** -37 + 60 * CPIX_MAX * 2.0 ** -45
+             + 1.3 * 2.0 ** -32)
+    assert 2.0 ** -28 < worst < BOUND_TURNS, worst
+
+
+def test_int_contraction_adversarial_worst_case():
+    """D = 60 at the range limits with every rounding error of the same
+    sign: Cq and cq both round by ~1/2 unit, signed so that every term
+    delta_C k + Cpix delta_k adds.  The error against the exact product of
+    the fp64 operands exceeds the old 2^-28 claim and stays below 2^-27."""
+    D = 60
+    cpix, turns = [], []
+    for d in range(D):
+        sign = 1.0 if d % 2 == 0 else -1.0
+        # k 2^44 = integer + 15/32 (k ~ 8 has 2^-5 resolution there): rint
+        # rounds it down, delta_k < 0, and with Cpix < 0 Cpix delta_k > 0
+        base = (127.0 * M6 - 1.0 if sign > 0 else -128.0 * M6 + 1.0) + 15.0 / 32.0
+        k = np.ldexp(base, -TAU)
+        assert np.ldexp(k, TAU) == base
+        # Cpix 2^36 = integer +- 31/64 so that rint moves it toward sign(k):
+        # delta_C k > 0
+        cb = np.floor(-(CPIX_MAX - 20.0 - d) * 2.0 ** SIGMA)
+        cb = cb + (1.0 - 31.0 / 64.0 if sign > 0 else 31.0 / 64.0)
+        c = np.ldexp(cb, -SIGMA)
+        assert np.ldexp(c, SIGMA) == cb
+        cpix.append(float(c))
+        turns.append(float(k))
+    R = int_phase_turns(cpix, turns)
+    exact = sum(Fraction(c) * Fraction(k) for c, k in zip(cpix, turns))
+    exact_frac = exact - round(exact)
+    err = abs(Fraction(R, 2 ** 32) - exact_frac)
+    err = float(min(err, 1 - err))
+    assert 2.0 ** -28 < err <= BOUND_TURNS, (err, np.log2(err))
