@@ -323,6 +323,30 @@ def test_tess_rejects_bad_labels():
 
 
 @pytest.mark.gpu
+def test_tess_label_check_not_fooled_by_reused_storage():
+    """The once-per-template label check is keyed on the tensor object: a
+    new, invalid label tensor in the freed block of a validated one (the
+    caching allocator hands it straight back, same size, same _version) is
+    checked again and refused."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from ska_sdp_screen_fitting_amd import get_context
+    dev = torch.device("cuda", 0)
+    ctx = get_context(0)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    ph = torch.zeros((2, 3), dtype=torch.float64, device=dev)
+    out = torch.empty((2, 4, 8, 8), dtype=torch.float32, device=dev)
+    good = torch.ones((8, 8), dtype=torch.int32, device=dev)
+    ctx.tess_fill(good, 8, 8, ph, 3, 2, out)
+    del good
+    # (normally the same storage block; refused either way)
+    bad = torch.full((8, 8), 9, dtype=torch.int32, device=dev)
+    with pytest.raises(ValueError):
+        ctx.tess_fill(bad, 8, 8, ph, 3, 2, out)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n,S", [(17, 70), (128, 45), (64, 33), (33, 1)])
 def test_tess_gather_amplitudes_nan_byteswap(n, S):
     """The unsmoothed table + gather-store kernels (float4 runs when
