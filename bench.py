@@ -913,6 +913,12 @@ def main():
         dev = torch.device("cuda", gpu)
     coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
     if world > 1 or args.force_dist:
+        # --force-dist without a launcher: a one-rank env:// rendezvous
+        for k, v in (("RANK", "0"), ("WORLD_SIZE", "1"), ("LOCAL_RANK", "0"),
+                     ("MASTER_ADDR", "127.0.0.1")):
+            os.environ.setdefault(k, v)
+        if "MASTER_PORT" not in os.environ:
+            os.environ["MASTER_PORT"] = str(_free_port())
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:

@@ -83,3 +83,17 @@ def test_world_size_mismatch_still_refused():
                         "--rehearse-cpu", "--dist-backend", "gloo"],
                        cwd=REPO, env=env, capture_output=True, text=True, timeout=120)
     assert p.returncode != 0 and "WORLD_SIZE=1" in p.stderr
+
+
+def test_force_dist_one_rank_without_launcher():
+    """--force-dist at N = 1 with no launcher: a one-rank env:// group, the
+    setup collectives run through it (on the GPU box: RCCL)."""
+    p = run_bench("--gpus", "1", "--dist-backend", "gloo", "--workload", "tiny",
+                  "--rehearse-cpu", "--force-dist")
+    assert p.returncode == 0, p.stderr[-2000:]
+    # (one process, no launcher to filter its stdout: gloo's own peer
+    # message shares it with the JSON line)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])["dist"]
+    assert d["backend"] == "gloo" and d["world"] == 1 and len(d["per_rank"]) == 1
