@@ -177,9 +177,10 @@ int sf_device_cus(sf_ctx* ctx, int* n_cu);
  * contraction.  |error| < 2^-27 turn of phase over the allowed ranges
  * (7.06e-9 turn at D = 60, |coef / 2 pi| = 8.03 turns, |Cpix| = 1905 with
  * every rounding aligned; ~2^-32 at the BASELINE configs), below the fp32
- * rounding of the reduced phase (up to 2^-26 turn); it runs in the register tile and the
- * LDS-staged kernels alike (same bits), SF_EVAL_KERNEL_SHB is replaced by the
- * register tile (sf_get_eval_kernel / sf_get_eval_contraction say so). */
+ * rounding of the reduced phase (up to 2^-26 turn); it runs in the register
+ * tile, the SHB tile (pixel digits shared in LDS by 4 waves) and the
+ * LDS-staged kernels alike (same bits; sf_get_eval_kernel /
+ * sf_get_eval_contraction say which). */
 #define SF_OPT_EVAL_INT 15
 #define SF_EVAL_KERNEL_AUTO 0
 #define SF_EVAL_KERNEL_TILE 1
@@ -189,7 +190,7 @@ int sf_device_cus(sf_ctx* ctx, int* n_cu);
 #define SF_EVAL_KERNEL_LDS8H 5 /* LDS-staged, 2 MFMA tiles per wave (large D) */
 #define SF_EVAL_KERNEL_LDS16H 6
 #define SF_EVAL_KERNEL_TILE3 7 /* register tile at 3 waves per SIMD */
-#define SF_EVAL_KERNEL_SHB 8 /* register tile, Cpix shared in LDS by 4 waves */
+#define SF_EVAL_KERNEL_SHB 8 /* register tile, Cpix (or its digits) shared in LDS by 4 waves */
 /* The evaluation kernel sf_kl_eval (gain = 0) or sf_kl_eval_gain (gain = 1)
  * runs for the current grid and these flags on a 16-byte aligned output
  * (one of SF_EVAL_KERNEL_TILE / _LDS4 / _LDS8 / _LDS16). */

@@ -149,11 +149,9 @@ int pick_eval_kernel(const sf_ctx* ctx, bool gain, unsigned flags,
   const bool lds_ok = !gain && (flags & SF_EVAL_FAST_SINCOS) &&
                       (ctx->n_pix % 4 == 0) && out_aligned16;
   const int opt = ctx->eval_kernel;
-  // the integer-digit contraction (phase D >= 45) runs on the register tile
-  // and the LDS-staged kernels (same bits); SHB keeps fp64 fragments in LDS
-  // and is replaced by the register tile there
+  // the integer-digit contraction (phase D >= 45) runs on the register tile,
+  // the SHB tile (pixel digits in LDS) and the LDS-staged kernels (same bits)
   const bool ic = eval_int_applies(ctx, gain, flags, out_aligned16);
-  if (ic && opt == SF_EVAL_KERNEL_SHB) return SF_EVAL_KERNEL_TILE;
   // (auto: the register tile -- 512^2 x D = 50 0.744 with 4-group items;
   // the LDS-staged shapes 0.66-0.70, profiles/round3y_eval_items_512.txt)
   if (ic && opt == SF_EVAL_KERNEL_AUTO) return SF_EVAL_KERNEL_TILE;

@@ -375,11 +375,16 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
   constexpr int kFrag = KS * kTiles * 64;  // Cpix doubles of a wave pixel block
   // IC: the integer-digit contraction (kl_eval_int.h) instead of the fp64
   // MFMAs; slots it cannot carry take the fp64 contraction with the Cpix
-  // fragments read from memory
-  static_assert(!IC || (FAST && !SHB && !GAIN), "integer contraction: fast phase register tile");
+  // fragments read from memory.  IC + SHB: the pixel digit fragments of the
+  // workgroup's 64-pixel block sit in LDS (24 KiB) instead of 96 VGPRs per
+  // wave, read one tile at a time (round 4: 3 waves / SIMD instead of 2)
+  static_assert(!IC || (FAST && !GAIN), "integer contraction: fast phase screens");
   // fixed-point phase reduction (kRevMagic) for D <= 44
   constexpr bool kMagic = FAST && KS <= kMagicMaxKS && !IC;
-  __shared__ double bsh[SHB ? kFrag : 1];
+  // SHB: the fp64 Cpix fragments, or (IC) the pixel digit fragments
+  // [digit][tile][lane] of the wave block (kDigits x kTiles x 64 x 16 B)
+  constexpr int kShDoubles = SHB ? (IC ? kDigits * kTiles * 64 * 2 : kFrag) : 1;
+  __shared__ double bsh[kShDoubles];
   const int l = threadIdx.x & 63;
   // wave index, wave-uniform: keeps slot / ring arithmetic on the SALU
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -394,8 +399,16 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
     const int64_t p0 = wpb * kWavePix + (int64_t)(l & 15) * kTiles;
     if constexpr (SHB) {
       __syncthreads();  // the previous item's reads of bsh are done
-      if (wpb * kWavePix < P)
-        for (int i = threadIdx.x; i < kFrag; i += 256) bsh[i] = cfrag[wpb * kFrag + i];
+      if (wpb * kWavePix < P) {
+        if constexpr (IC) {
+          constexpr int kN = kDigits * kTiles * 64;
+          v4i* dst = reinterpret_cast<v4i*>(bsh);
+          const v4i* src = dg.cdig + wpb * kN;
+          for (int i = threadIdx.x; i < kN; i += 256) dst[i] = src[i];
+        } else {
+          for (int i = threadIdx.x; i < kFrag; i += 256) bsh[i] = cfrag[wpb * kFrag + i];
+        }
+      }
       __syncthreads();
     }
     if (wpb * kWavePix >= P) continue;
@@ -408,9 +421,10 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
         for (int t = 0; t < kTiles; ++t)
           bf[kk][t] = cfrag[((wpb * KS + kk) * kTiles + t) * 64 + l];
     }
-    // IC: the pixel digit fragments [tile][digit]
-    v4i bd[kTiles][IC ? kDigits : 1];
-    if constexpr (IC) {
+    // IC: the pixel digit fragments [tile][digit] (IC + SHB: read per tile
+    // from LDS in the group loop instead)
+    v4i bd[kTiles][IC && !SHB ? kDigits : 1];
+    if constexpr (IC && !SHB) {
 #pragma unroll
       for (int t = 0; t < kTiles; ++t)
 #pragma unroll
@@ -462,16 +476,19 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
       okp = s >= S || f != 0;
     };
     if constexpr (IC) {
-      dig_load(wp, dg.kdig, slot_base + rs, S, l);
-      load_flag(slot_base + rs);
+      const int64_t sw = slot_base + (SHB ? w : 0) * 16;
+      dig_load(wp, dg.kdig, sw + rs, S, l);
+      load_flag(sw + rs);
       // everything loaded so far must have landed before the group loop (as
       // the Cpix fragments below): else the compiler, merging this path with
       // the loop's back edge, waits at the loop top with a count that covers
       // the previous group's stores as well
+      if constexpr (!SHB) {
 #pragma unroll
-      for (int t = 0; t < kTiles; ++t)
+        for (int t = 0; t < kTiles; ++t)
 #pragma unroll
-        for (int i = 0; i < kDigits; ++i) asm volatile("" ::"v"(bd[t][i]));
+          for (int i = 0; i < kDigits; ++i) asm volatile("" ::"v"(bd[t][i]));
+      }
 #pragma unroll
       for (int n = 0; n < kDigits; ++n) asm volatile("" ::"v"(wp.w[n]));
       asm volatile("" ::"s"(__builtin_amdgcn_ballot_w64(okp)));
@@ -573,7 +590,16 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
         const int rowbit = 4 * (l >> 4);
 #pragma unroll
         for (int t = 0; t < kTiles; ++t) {
-          const v4i R = dig_contract(wp, bd[t]);
+          v4i R;
+          if constexpr (SHB) {
+            const v4i* bs = reinterpret_cast<const v4i*>(bsh);
+            v4i bt[kDigits];
+#pragma unroll
+            for (int i = 0; i < kDigits; ++i) bt[i] = bs[(i * kTiles + t) * 64 + l];
+            R = dig_contract(wp, bt);
+          } else {
+            R = dig_contract(wp, bd[t]);
+          }
 #pragma unroll
           for (int r = 0; r < 4; ++r) frg[r][t] = (float)R[r] * kTwoM32;
         }
@@ -1399,6 +1425,64 @@ int launch_eval_int(sf_ctx* ctx, const double* coef, int64_t S_all, float* out,
   return SF_OK;
 }
 
+// The integer-digit contraction on the SHB tile (SF_EVAL_KERNEL_SHB with the
+// integer contraction): the 4 waves of a workgroup share one 64-pixel block,
+// its pixel digits in LDS, and take its 16-slot groups round-robin
+template <int KS>
+int launch_eval_int_shb(sf_ctx* ctx, const double* coef, int64_t S_all, float* out,
+                        int64_t ring, unsigned flags, unsigned* sums) {
+  const int64_t P = ctx->n_pix;
+  const int64_t n_wpb = ctx->n_pix_blocks * kEvalWaves;
+  // groups per item: 4 per wave (the register tile's 4-group items)
+  const int groups = eval_chunk_groups(n_wpb, S_all, ctx->eval_groups ? ctx->eval_groups : 16, 4096);
+  const int64_t gs = 16 * (int64_t)groups;
+  int64_t per = eval_launch_slots(ctx, n_wpb, groups, 256);
+  const int64_t cap = kDigChunk < gs ? gs : (kDigChunk / gs) * gs;
+  if (per > cap) per = cap;
+  {
+    const int rc = ensure_kdig(ctx, S_all < per ? S_all : per);
+    if (rc != SF_OK) return rc;
+  }
+  // pixel bands as the register tile's (bands of 128 x 256 pixels)
+  const int64_t n_pb = ctx->n_pix_blocks;
+  const int auto_bands = n_pb >= 1024 ? (int)(n_pb / 128 < 128 ? n_pb / 128 : 128) : 1;
+  unsigned fl = flags | eval_band_flags(ctx, n_wpb, auto_bands);
+  if (ctx->eval_xcd_map < 0 && ctx->eval_bands == 0 && auto_bands > 1)
+    fl |= kEvalXcdInterleave;
+  const bool nt = flags & SF_EVAL_NT_STORES;
+  const bool be = flags & SF_EVAL_BIG_ENDIAN;
+  for (int64_t b = 0; b < S_all; b += per) {
+    const int64_t S = S_all - b < per ? S_all - b : per;
+    const double* cb = coef + b * ctx->D;
+    unsigned* sb = sums ? sums + b : nullptr;
+    {
+      const int rc = run_kdig(ctx, cb, S);
+      if (rc != SF_OK) return rc;
+    }
+    const int64_t nsc = (S + gs - 1) / gs;
+    const unsigned nblk = (unsigned)eval_grid(ctx, n_wpb, nsc, 256);
+#define SF_LAUNCH_ICS(N, B)                                                              \
+  hipLaunchKernelGGL((kl_eval_kernel<KS, 3, true, true, N, false, true, B, false, true>), \
+                     dim3(nblk), dim3(256), 0, ctx->stream, ctx->d_cfrag, cb, nullptr,   \
+                     nullptr, ctx->D, S, P, n_wpb, nsc, groups, out, ring, b % ring, fl, \
+                     sb, ctx->d_trash, ctx->rev_thr, dig_args(ctx, 0))
+    if constexpr (KS >= 12) {
+      if (nt) {
+        if (be) SF_LAUNCH_ICS(true, 1); else SF_LAUNCH_ICS(true, 0);
+      } else {
+        if (be) SF_LAUNCH_ICS(false, 1); else SF_LAUNCH_ICS(false, 0);
+      }
+    }
+#undef SF_LAUNCH_ICS
+    SF_HIP(hipGetLastError());
+    {
+      const int rc = kdig_done(ctx);
+      if (rc != SF_OK) return rc;
+    }
+  }
+  return SF_OK;
+}
+
 template <int KS>
 int launch_eval_pick(sf_ctx* ctx, const double* coef, const double* cxx,
                             const double* cyy, int64_t S, float* out,
@@ -1408,9 +1492,12 @@ int launch_eval_pick(sf_ctx* ctx, const double* coef, const double* cxx,
   const int v = pick_eval_kernel(ctx, cxx != nullptr, flags, aligned);
   // the integer-digit contraction: the LDS-staged kernels take it themselves,
   // the register tile through launch_eval_int
-  if (eval_int_applies(ctx, cxx != nullptr, flags, aligned) &&
-      (v == SF_EVAL_KERNEL_TILE || v == SF_EVAL_KERNEL_TILE3))
-    return launch_eval_int<KS>(ctx, coef, S, out, ring, flags, sums);
+  if (eval_int_applies(ctx, cxx != nullptr, flags, aligned)) {
+    if (v == SF_EVAL_KERNEL_TILE || v == SF_EVAL_KERNEL_TILE3)
+      return launch_eval_int<KS>(ctx, coef, S, out, ring, flags, sums);
+    if (v == SF_EVAL_KERNEL_SHB)
+      return launch_eval_int_shb<KS>(ctx, coef, S, out, ring, flags, sums);
+  }
   switch (v) {
     case SF_EVAL_KERNEL_LDS4:
       return launch_eval_lds<KS, 4, 4>(ctx, coef, S, out, ring, flags, sums);

@@ -88,13 +88,14 @@ def test_int_phase_vs_fp64_and_oracle(ctx, dev, n_dir, grid):
     coef[31, 0] = np.inf
     fb = [3, 9, 31]                      # the fp64 rows
     flags = 1 | SF_EVAL_FAST_SINCOS
-    # auto: the register tile; SHB (fp64 fragments in LDS) is replaced by it;
+    # auto: the register tile; SHB holds the pixel digits in LDS (round 4);
     # the LDS-staged kernels take the integer contraction too -- every kernel
     # writes the same bits (below)
     try:
         assert ctx.eval_kernel(flags) == "kl_eval_kernel"
         ctx.set_option(SF_OPT_EVAL_KERNEL, SF_EVAL_KERNEL_SHB)
-        assert ctx.eval_kernel(flags) == "kl_eval_kernel"
+        assert ctx.eval_kernel(flags) == "kl_eval_kernel<Cpix in LDS>"
+        assert ctx.eval_contraction(flags) == "i8-digits"
     finally:
         ctx.set_option(SF_OPT_EVAL_KERNEL, SF_EVAL_KERNEL_AUTO)
     oi = run(ctx, dev, [coef], S, grid, True, flags)
