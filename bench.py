@@ -908,7 +908,12 @@ def main():
         gpu, dev = None, torch.device("cpu")
     else:
         n_dev = torch.cuda.device_count()
-        gpu = local_rank if args.dist_backend == "nccl" else local_rank % max(n_dev, 1)
+        # local rank -> visible device; modulo, so a launcher that gives every
+        # rank its own one-device HIP_VISIBLE_DEVICES works too (two ranks
+        # that resolve to one card are refused below under nccl)
+        if n_dev < 1:
+            raise SystemExit("bench.py: no GPU visible (torch.cuda.device_count() == 0)")
+        gpu = local_rank % n_dev
         torch.cuda.set_device(gpu)
         dev = torch.device("cuda", gpu)
     coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
