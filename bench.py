@@ -88,7 +88,7 @@ def parse():
                          "stream (pipelined mode); -1 (default): 16 when "
                          "D <= 32 (the fit then runs on exactly those), else 0 "
                          "(at D = 50 the eval is compute-bound and the fit "
-                         "too heavy for 16 CUs: config 5 +8 %)")
+                         "too heavy for 16 CUs: config 5 +8 %%)")
     ap.add_argument("--fit-on-reserved", type=int, default=-1,
                     help="1: confine the fit stream to the reserved CUs "
                          "(pipelined mode); -1 (default): when D <= 32, where "
@@ -153,9 +153,10 @@ def parse():
     ap.add_argument("--launch-timeout", type=float, default=3000.0,
                     help="--gpus N without a launcher: seconds before the "
                          "self-launched ranks are killed")
-    ap.add_argument("--no-config5-leg", action="store_true",
-                    help="skip the one-step config-5 side leg of the default "
-                         "N = 1 run")
+    ap.add_argument("--no-child-legs", "--no-config5-leg", action="store_true",
+                    dest="no_child_legs",
+                    help="skip the child-process legs of the default N = 1 run "
+                         "(config 5, gain and tessellated on the config-3 shape)")
     return ap.parse_args()
 
 
@@ -673,43 +674,67 @@ def side_legs(ctx, torch, dev, stream, fit_stream, fit, evaluate, coef, bounds,
     return res
 
 
-def config5_leg(timeout_s=420):
-    """BASELINE.json configs[4] (SKA-Low scale) beside the config-4 line: one
-    timed step (after one warmup step) of the shard one of its 8 GPUs runs --
-    64 of 512 stations x 4000 t x 64 f x 50 dir = 16.4 M slots, KL 512^2,
-    fit + eval, integer-digit contraction, discard + checksum mode
-    (kl_screen.py:411-449) -- in a child ``bench.py --workload config5``
-    (its own device buffers, ~45 GB), with its sampled-slot parity and
-    streamed-checksum checks."""
+def child_leg(extra, what, timeout_s=420):
+    """One workload of BASELINE.json beside the config-4 line, in a child
+    ``bench.py`` (its own device buffers; the parent holds its own and is
+    idle meanwhile): its value, eval roofline, checks and wall time."""
     import subprocess
     cmd = [sys.executable, os.path.abspath(__file__), "--gpus", "1",
-           "--workload", "config5", "--steps", "1", "--warmup", "1",
-           "--no-cpu-baseline", "--no-fits", "--no-side-legs", "--no-config5-leg"]
+           "--no-cpu-baseline", "--no-fits", "--no-side-legs", "--no-child-legs"] + extra
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     t0 = time.perf_counter()
     try:
         p = subprocess.run(cmd, env=env, capture_output=True, text=True,
                            timeout=timeout_s)
     except subprocess.TimeoutExpired:
-        return {"error": f"timed out after {timeout_s} s"}
+        return {"error": f"timed out after {timeout_s} s", "args": extra}
     wall = time.perf_counter() - t0
     if p.returncode != 0:
-        return {"error": f"exit {p.returncode}: {p.stderr[-600:]}"}
+        return {"error": f"exit {p.returncode}: {p.stderr[-600:]}", "args": extra}
     r = json.loads(p.stdout.strip().splitlines()[-1])
-    rf, sm = r["roofline"], r["check"]["sampled_slots"]
-    return {
-        "workload": r["config"]["workload"],
+    rf, chk = r["roofline"], r["check"]
+    sm = chk.get("sampled_slots") or {}
+    out = {
+        "workload": r["config"]["workload"], "args": " ".join(extra),
         "value": r["value"], "unit": r["unit"], "steps": r["steps"],
         "warmup": r["warmup"], "ms_per_step": r["ms_per_step"],
-        "dtype": r["dtype"], "stages_ms": r["stages_ms"],
+        "dtype": r["dtype"], "stages_ms": r.get("stages_ms"),
         "kernel": rf["kernel"], "launch_ms": rf["launch_ms"],
         "bytes_per_launch": rf["bytes_per_launch"], "achieved_GBs": rf["achieved"],
         "frac": rf["frac"], "traffic": rf["traffic"], "mfma": r.get("mfma"),
-        "sampled_slots": sm, "checksums_match": sm.get("checksums_match"),
-        "max_abs_err_vs_fp64": sm["max_abs_err_vs_fp64"], "ok": sm["ok"],
-        "child_wall_s": wall,
-        "what": ("one step of config 5's per-GPU shard in a child process "
-                 "(bench.py --workload config5 --steps 1 --warmup 1)")}
+        "check": chk, "child_wall_s": wall, "what": what}
+    if sm:
+        out.update(sampled_slots=sm, checksums_match=sm.get("checksums_match"),
+                   max_abs_err_vs_fp64=sm["max_abs_err_vs_fp64"], ok=sm["ok"])
+    return out
+
+
+def child_legs():
+    """The default line's other BASELINE.json workloads, each observed by
+    the same command as the headline:
+
+    * config5: BASELINE.json configs[4] (SKA-Low scale), one timed step
+      (after one warmup step) of the shard one of its 8 GPUs runs -- 64 of
+      512 stations x 4000 t x 64 f x 50 dir = 16.4 M slots, KL 512^2, fit +
+      eval on the integer-digit contraction, discard + checksum mode
+      (kl_screen.py:411-449), ~45 GB of device buffers;
+    * gain_config3: the gain screens (phase + XX / YY amplitude fits, the
+      three-contraction eval with 10 **, kl_screen.py:96-125, 319-378) on
+      the config-3 shape, 5 steps;
+    * tess_config3: the tessellated fill (voronoi_screen.py:132-216) on the
+      config-3 shape, 10 steps."""
+    return {
+        "config5": child_leg(
+            ["--workload", "config5", "--steps", "1", "--warmup", "1"],
+            "one step of config 5's per-GPU shard in a child process "
+            "(bench.py --workload config5 --steps 1 --warmup 1)"),
+        "gain_config3": child_leg(
+            ["--screen", "gain", "--workload", "config3", "--steps", "5", "--warmup", "1"],
+            "gain screens on the config-3 shape in a child process"),
+        "tess_config3": child_leg(
+            ["--screen", "tess", "--workload", "config3", "--steps", "10", "--warmup", "2"],
+            "tessellated fill on the config-3 shape in a child process"),
+    }
 
 
 def rehearse_cpu(args, dist, world, rank, sol, setup, A, A_total, a0):
@@ -1211,10 +1236,10 @@ def main():
         side = side_legs(ctx, torch, dev, stream, first_fit_stream, fit, evaluate,
                          coef, bounds, F, A, D, P, out, ring, flags, gain, amp)
     if (rank == 0 and world == 1 and args.workload == "config4" and not gain
-            and not args.no_config5_leg and not args.as_shard_of
+            and not args.no_child_legs and not args.as_shard_of
             and not args.eval_only):
-        log("config-5 leg (child process)")
-        side["config5"] = config5_leg()
+        log("child legs: config 5, gain and tessellated on config 3")
+        side.update(child_legs())
 
     if rank == 0:
         # SURVEY.md §8(d), per step; gain screens read three coefficient sets
