@@ -182,6 +182,10 @@ int sf_device_cus(sf_ctx* ctx, int* n_cu);
  * LDS-staged kernels alike (same bits; sf_get_eval_kernel /
  * sf_get_eval_contraction say which). */
 #define SF_OPT_EVAL_INT 15
+/* SF_OPT_EVAL_WG_WAVES: waves per workgroup of the integer-digit register
+ * tile -- 4 (0 = default: 256 pixels, 1 KiB store runs per (slot, plane)) or
+ * 8 (512 pixels, 2 KiB runs).  Same bits. */
+#define SF_OPT_EVAL_WG_WAVES 16
 #define SF_EVAL_KERNEL_AUTO 0
 #define SF_EVAL_KERNEL_TILE 1
 #define SF_EVAL_KERNEL_LDS4 2

@@ -231,6 +231,11 @@ int sf_set_option(sf_ctx* ctx, int option, int value) {
                  "sf_set_option: eval int must be -1 or 0");
       ctx->eval_int = value;
       return SF_OK;
+    case SF_OPT_EVAL_WG_WAVES:
+      SF_REQUIRE(value == 0 || value == 4 || value == 8, SF_EINVAL,
+                 "sf_set_option: eval workgroup waves must be 0, 4 or 8");
+      ctx->eval_wg_waves = value;
+      return SF_OK;
     default:
       set_error("sf_set_option: unknown option");
       return SF_EINVAL;

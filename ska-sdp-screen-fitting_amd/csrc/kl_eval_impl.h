@@ -363,9 +363,12 @@ __device__ __forceinline__ float amp2f(double log2a) {
 // lane_base + 16 r P -- one base per group instead of, per row, a ring index,
 // a 64-bit product and the trash select (a run-time choice between the two
 // would again be a branch round the stores, see BEM)
+// NWV: waves per workgroup (the workgroup's pixel block is NWV x 64 pixels;
+// the integer tile can run 8, SF_OPT_EVAL_WG_WAVES)
 template <int KS, int MINW, bool VEC4, bool FAST, bool NT, bool GAIN,
-          bool SHB = false, int BEM = 2, bool DIRECT = false, bool IC = false>
-__global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
+          bool SHB = false, int BEM = 2, bool DIRECT = false, bool IC = false,
+          int NWV = kEvalWaves>
+__global__ __launch_bounds__(64 * NWV, MINW) void kl_eval_kernel(
     const double* __restrict__ cfrag, const double* __restrict__ coef,
     const double* __restrict__ coef_xx, const double* __restrict__ coef_yy,
     int D, int64_t S, int64_t P, int64_t n_pb, int64_t n_sc, int chunk_groups,
@@ -379,6 +382,7 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
   // workgroup's 64-pixel block sit in LDS (24 KiB) instead of 96 VGPRs per
   // wave, read one tile at a time (round 4: 3 waves / SIMD instead of 2)
   static_assert(!IC || (FAST && !GAIN), "integer contraction: fast phase screens");
+  static_assert(NWV == kEvalWaves || (IC && !SHB), "8-wave workgroups: integer register tile");
   // fixed-point phase reduction (kRevMagic) for D <= 44
   constexpr bool kMagic = FAST && KS <= kMagicMaxKS && !IC;
   // SHB: the fp64 Cpix fragments, or (IC) the pixel digit fragments
@@ -395,7 +399,7 @@ __global__ __launch_bounds__(256, MINW) void kl_eval_kernel(
     int64_t pb, sc;
     eval_block(bb, n_pb, n_sc, pb, sc, flags);
     if (sc >= n_sc) continue;  // uniform per workgroup
-    const int64_t wpb = SHB ? pb : pb * kEvalWaves + w;
+    const int64_t wpb = SHB ? pb : pb * NWV + w;
     const int64_t p0 = wpb * kWavePix + (int64_t)(l & 15) * kTiles;
     if constexpr (SHB) {
       __syncthreads();  // the previous item's reads of bsh are done
@@ -1364,29 +1368,36 @@ int launch_eval_lds(sf_ctx* ctx, const double* coef, int64_t S_all,
   return SF_OK;
 }
 
-// The register tile on the integer-digit contraction (phase, D >= 45)
-template <int KS>
-int launch_eval_int(sf_ctx* ctx, const double* coef, int64_t S_all, float* out,
-                    int64_t ring, unsigned flags, unsigned* sums) {
+// The register tile on the integer-digit contraction (phase, D >= 45);
+// NWV = 4 (256-pixel workgroup blocks) or 8 (512, SF_OPT_EVAL_WG_WAVES)
+template <int KS, int NWV>
+int launch_eval_int_nw(sf_ctx* ctx, const double* coef, int64_t S_all, float* out,
+                       int64_t ring, unsigned flags, unsigned* sums) {
   const int64_t P = ctx->n_pix;
-  const int64_t n_pb = ctx->n_pix_blocks;
+  constexpr int kThreads = 64 * NWV;
+  // workgroup pixel blocks of NWV x 64 pixels (the wave blocks of the Cpix /
+  // digit fragments are 64 pixels either way)
+  const int64_t n_pb = (ctx->n_pix_blocks * kEvalWaves + NWV - 1) / NWV;
+  const int64_t n_pb256 = ctx->n_pix_blocks;
   // large grids (>= 1024 blocks of 256 px: 512^2 and up): items of 4 groups
   // (the digit fragments are 6 KB per wave block, a quarter of the fp64 ones,
   // so short items cost little reload): 512^2 x D = 50 0.691 (64 groups) ->
   // 0.744 of 8 TB/s, 2 / 8 groups 0.723 / 0.731
   // (profiles/round3y_eval_items_512.txt)
-  const int def_groups = n_pb >= 1024 ? 4 : 64;
-  const int groups = eval_chunk_groups(n_pb, S_all, ctx->eval_groups ? ctx->eval_groups : def_groups, 2048);
+  const int def_groups = n_pb256 >= 1024 ? 4 : 64;
+  const int groups = eval_chunk_groups(n_pb, S_all, ctx->eval_groups ? ctx->eval_groups : def_groups,
+                                       2048 * kEvalWaves / NWV);
   const int64_t gs = 16 * (int64_t)groups;
-  int64_t per = eval_launch_slots(ctx, n_pb, groups, 256);
+  int64_t per = eval_launch_slots(ctx, n_pb, groups, kThreads);
   const int64_t cap = kDigChunk < gs ? gs : (kDigChunk / gs) * gs;
   if (per > cap) per = cap;
   {
     const int rc = ensure_kdig(ctx, S_all < per ? S_all : per);
     if (rc != SF_OK) return rc;
   }
-  // bands / XCD map as the fp64 register tile (launch_eval_ks)
-  const int auto_bands = n_pb >= 1024 ? (int)(n_pb / 128 < 128 ? n_pb / 128 : 128) : 1;
+  // bands / XCD map as the fp64 register tile (launch_eval_ks): bands of
+  // 128 x 256 pixels
+  const int auto_bands = n_pb256 >= 1024 ? (int)(n_pb256 / 128 < 128 ? n_pb256 / 128 : 128) : 1;
   unsigned fl = flags | eval_band_flags(ctx, n_pb, auto_bands);
   if (ctx->eval_xcd_map < 0 && ctx->eval_bands == 0 && auto_bands > 1)
     fl |= kEvalXcdInterleave;
@@ -1402,11 +1413,11 @@ int launch_eval_int(sf_ctx* ctx, const double* coef, int64_t S_all, float* out,
     }
     // (direct addressing: measured 2 % slower at D = 50 with fp64, not used)
     const int64_t nsc = (S + gs - 1) / gs;
-    const unsigned nblk = (unsigned)eval_grid(ctx, n_pb, nsc, 256);
-#define SF_LAUNCH_IC(N, B)                                                          \
-  hipLaunchKernelGGL((kl_eval_kernel<KS, 2, true, true, N, false, false, B, false, true>), \
-                     dim3(nblk), dim3(256), 0, ctx->stream, ctx->d_cfrag, cb, nullptr,     \
-                     nullptr, ctx->D, S, P, n_pb, nsc, groups, out, ring, b % ring, fl,    \
+    const unsigned nblk = (unsigned)eval_grid(ctx, n_pb, nsc, kThreads);
+#define SF_LAUNCH_IC(N, B)                                                                 \
+  hipLaunchKernelGGL((kl_eval_kernel<KS, 2, true, true, N, false, false, B, false, true, NWV>), \
+                     dim3(nblk), dim3(kThreads), 0, ctx->stream, ctx->d_cfrag, cb, nullptr,     \
+                     nullptr, ctx->D, S, P, n_pb, nsc, groups, out, ring, b % ring, fl,         \
                      sb, ctx->d_trash, ctx->rev_thr, dig_args(ctx, 0))
     if constexpr (KS >= 12) {
       if (nt) {
@@ -1423,6 +1434,14 @@ int launch_eval_int(sf_ctx* ctx, const double* coef, int64_t S_all, float* out,
     }
   }
   return SF_OK;
+}
+
+template <int KS>
+int launch_eval_int(sf_ctx* ctx, const double* coef, int64_t S_all, float* out,
+                    int64_t ring, unsigned flags, unsigned* sums) {
+  if (ctx->eval_wg_waves == 8)
+    return launch_eval_int_nw<KS, 8>(ctx, coef, S_all, out, ring, flags, sums);
+  return launch_eval_int_nw<KS, kEvalWaves>(ctx, coef, S_all, out, ring, flags, sums);
 }
 
 // The integer-digit contraction on the SHB tile (SF_EVAL_KERNEL_SHB with the

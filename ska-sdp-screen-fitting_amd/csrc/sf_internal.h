@@ -69,6 +69,7 @@ struct sf_ctx {
   int8_t* d_cdig = nullptr;    // [wave pixel blocks][6][kTiles][64][16 B]
   int dig_ok = 0;              // 1: max |Cpix| * 2^36 fits 6 digits
   int eval_int = -1;           // SF_OPT_EVAL_INT (-1 auto, 0 off)
+  int eval_wg_waves = 0;       // SF_OPT_EVAL_WG_WAVES (0 = 4, or 8)
   // per-call slot digits of the integer contraction (kl_kdig_kernel)
   int8_t* d_kdig = nullptr;    // [slot][6][64]
   uint8_t* d_kflag = nullptr;  // [slot]: 1 = integer path

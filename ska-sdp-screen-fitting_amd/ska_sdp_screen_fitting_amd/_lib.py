@@ -36,6 +36,7 @@ SF_OPT_TESS_WAVES = 12
 SF_OPT_TESS_TILE = 13
 SF_OPT_TESS_BOX = 14
 SF_OPT_EVAL_INT = 15
+SF_OPT_EVAL_WG_WAVES = 16
 SF_EVAL_KERNEL_AUTO = 0
 SF_EVAL_KERNEL_TILE = 1
 SF_EVAL_KERNEL_LDS4 = 2

@@ -99,13 +99,20 @@ def test_int_phase_vs_fp64_and_oracle(ctx, dev, n_dir, grid):
     finally:
         ctx.set_option(SF_OPT_EVAL_KERNEL, SF_EVAL_KERNEL_AUTO)
     oi = run(ctx, dev, [coef], S, grid, True, flags)
+    from ska_sdp_screen_fitting_amd._lib import SF_OPT_EVAL_WG_WAVES
     try:
         for kv in sorted(EVAL_KERNEL_NAMES):
             ctx.set_option(SF_OPT_EVAL_KERNEL, kv)
             o = run(ctx, dev, [coef], S, grid, True, flags)
             assert np.array_equal(o.view(np.int32), oi.view(np.int32)), kv
+        # the register tile with 8-wave (512-pixel) workgroups
+        ctx.set_option(SF_OPT_EVAL_KERNEL, SF_EVAL_KERNEL_TILE)
+        ctx.set_option(SF_OPT_EVAL_WG_WAVES, 8)
+        o = run(ctx, dev, [coef], S, grid, True, flags)
+        assert np.array_equal(o.view(np.int32), oi.view(np.int32)), "8 waves"
     finally:
         ctx.set_option(SF_OPT_EVAL_KERNEL, SF_EVAL_KERNEL_AUTO)
+        ctx.set_option(SF_OPT_EVAL_WG_WAVES, 0)
     try:
         ctx.set_option(SF_OPT_EVAL_KERNEL, SF_EVAL_KERNEL_TILE)
         of = run(ctx, dev, [coef], S, grid, False, flags)

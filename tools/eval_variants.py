@@ -22,7 +22,7 @@ from ska_sdp_screen_fitting_amd._lib import (  # noqa: E402
     SF_EVAL_KERNEL_LDS16H, SF_EVAL_KERNEL_SHB, SF_EVAL_KERNEL_TILE, SF_EVAL_KERNEL_TILE3,
     SF_EVAL_NAN_SCRUB, SF_EVAL_NT_STORES, SF_OPT_EVAL_KERNEL,
     SF_OPT_EVAL_GROUPS, SF_OPT_EVAL_KS_PAD, SF_OPT_EVAL_SLEEP,
-    SF_OPT_EVAL_XCD_MAP, SF_OPT_EVAL_BANDS, SF_OPT_EVAL_INT)
+    SF_OPT_EVAL_XCD_MAP, SF_OPT_EVAL_BANDS, SF_OPT_EVAL_INT, SF_OPT_EVAL_WG_WAVES)
 
 KERNELS = {"auto": SF_EVAL_KERNEL_AUTO, "tile": SF_EVAL_KERNEL_TILE,
            "tile3": SF_EVAL_KERNEL_TILE3,
@@ -50,7 +50,7 @@ for v in args.variants.split(","):
     # library's auto choice unless +xi (interleaved) / +xc (contiguous);
     # +int0: the fp64 contraction where the integer-digit one would apply
     k, *mods = v.split("+")
-    fl, pad, sleep, xi, grp, bands, ival = base, 0, 0, -1, 0, 0, -1
+    fl, pad, sleep, xi, grp, bands, ival, wgw = base, 0, 0, -1, 0, 0, -1, 0
     for m in mods:
         if m == "nt":
             fl |= SF_EVAL_NT_STORES
@@ -64,18 +64,21 @@ for v in args.variants.split(","):
             xi = 0
         elif m == "int0":
             ival = 0
+        elif m.startswith("w"):
+            wgw = int(m[1:])
         elif m.startswith("b"):
             bands = int(m[1:])
         elif m.startswith("g"):
             grp = int(m[1:])
         else:
             raise SystemExit(f"unknown variant modifier {m}")
-    variants[v] = (KERNELS[k], fl, (pad, sleep, xi, grp, bands, ival))
+    variants[v] = (KERNELS[k], fl, (pad, sleep, xi, grp, bands, ival, wgw))
 
 
-def use(kv, opts=(0, 0, -1, 0, 0, -1)):
-    pad, sleep, xi, grp, bands, ival = opts
+def use(kv, opts=(0, 0, -1, 0, 0, -1, 0)):
+    pad, sleep, xi, grp, bands, ival, wgw = opts
     ctx.set_option(SF_OPT_EVAL_INT, ival)
+    ctx.set_option(SF_OPT_EVAL_WG_WAVES, wgw)
     ctx.set_option(SF_OPT_EVAL_BANDS, bands)
     ctx.set_option(SF_OPT_EVAL_GROUPS, grp)
     ctx.set_option(SF_OPT_EVAL_KERNEL, kv)
