@@ -8,7 +8,7 @@ fp64 MFMA contraction of the same library (SF_OPT_EVAL_INT = 0):
 
 * finite slots: |d| <= 2e-6 vs the oracle (the fast-epilogue tolerance of
   every evaluation test), <= 3e-7 vs the fp64 contraction (phase error
-  <= 2^-28 turn plus one fp32 rounding of the reduced phase either way);
+  < 2^-27 turn plus one fp32 rounding of the reduced phase either way);
 * slots the digits cannot carry (NaN / Inf, |coef / 2 pi| beyond ~7.9 turns)
   take the fp64 contraction inside the same launch: bit for bit the fp64
   register tile's output;
@@ -196,3 +196,42 @@ def test_int_many_launches_checksums(ctx, dev):
         ctx.eval_sums(part, b - a, o, s2, b - a, flags=flags)
         torch.cuda.synchronize()
         assert torch.equal(s2, sums[a:b]), (a, b)
+
+
+def test_int_launches_on_two_streams(ctx, dev):
+    """Two integer-contraction calls on one context, issued on two streams
+    without a host sync between them: the second call's digit prepass
+    rewrites the context's slot-digit buffer only after the first call's
+    kernel has read it (the kdig_read event), so both results equal the
+    same calls run one after the other."""
+    from ska_sdp_screen_fitting_amd._lib import SF_EVAL_FAST_SINCOS, SF_EVAL_NAN_SCRUB
+    D, grid = 50, 64
+    pp, x, y = grid_for(D, grid, seed=13)
+    ctx.set_basis(pp)
+    ctx.set_grid(x, y)
+    flags = SF_EVAL_NAN_SCRUB | SF_EVAL_FAST_SINCOS
+    assert ctx.eval_contraction(flags) == "i8-digits"
+    S = 20000
+    g = torch.Generator(device=dev)
+    g.manual_seed(21)
+    ca = torch.randn((S, D), generator=g, device=dev, dtype=torch.float64) * 0.01
+    cb = torch.randn((S, D), generator=g, device=dev, dtype=torch.float64) * 0.02
+    want = []
+    for c in (ca, cb):
+        o = torch.empty((S, 4, grid, grid), dtype=torch.float32, device=dev)
+        ctx.eval(c, S, o, S, flags)
+        torch.cuda.synchronize()
+        want.append(o)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    outs = [torch.full((S, 4, grid, grid), -5.0, dtype=torch.float32, device=dev)
+            for _ in range(2)]
+    torch.cuda.synchronize()
+    try:
+        for st, c, o in ((s1, ca, outs[0]), (s2, cb, outs[1])):
+            ctx.set_stream(st.cuda_stream)
+            ctx.eval(c, S, o, S, flags)
+        torch.cuda.synchronize()
+    finally:
+        ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    for got, w in zip(outs, want):
+        assert torch.equal(got.view(torch.int32), w.view(torch.int32))
