@@ -6,7 +6,7 @@ out=$1; shift
 mkdir -p $out
 ( timeout -k 10 120 python3 bench.py "$@" > $out/bench.json 2> $out/bench.err ) &
 pid=$!
-sleep 8
+sleep ${PROBE_DELAY:-8}
 for i in 1 2 3 4 5 6; do
   timeout 10 rocm-smi --showpower --showclocks --showtemp >> $out/smi.txt 2>&1
   timeout 10 amd-smi metric -p -c 2>/dev/null | head -40 >> $out/amdsmi.txt
