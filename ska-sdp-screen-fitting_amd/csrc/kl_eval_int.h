@@ -51,7 +51,14 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 
 constexpr int kSigma = 36;       // Cq = rint(Cpix * 2^36)
 constexpr int kTauPhase = 44;    // cq = rint(coef / 2 pi * 2^44)
-constexpr int kDiagLo = 4;       // lowest diagonal kept
+#ifndef SF_DIG_ORDER
+#define SF_DIG_ORDER 0
+#endif
+#ifndef SF_DIAG_LO
+#define SF_DIAG_LO 4
+#endif
+constexpr int kDiagLo = SF_DIAG_LO;  // lowest diagonal kept (4 or 5)
+static_assert(kDiagLo == 4 || kDiagLo == 5, "kept diagonals: 4..9 or 5..9");
 constexpr int kDiagHi = 9;       // highest diagonal below a whole turn
 constexpr int kNDiag = kDiagHi - kDiagLo + 1;
 
@@ -137,6 +144,7 @@ __device__ __forceinline__ v4i dig_contract(const DigRows& r, const v4i (&bd)[kD
   v4i acc[kNDiag];
 #pragma unroll
   for (int k = 0; k < kNDiag; ++k) acc[k] = v4i{0, 0, 0, 0};
+#if SF_DIG_ORDER == 0
   // pixel digit outer: consecutive MFMAs feed different accumulators
 #pragma unroll
   for (int i = 0; i < kDigits; ++i)
@@ -145,10 +153,25 @@ __device__ __forceinline__ v4i dig_contract(const DigRows& r, const v4i (&bd)[kD
       if (k - i >= 0 && k - i < kDigits)
         acc[k - kDiagLo] = __builtin_amdgcn_mfma_i32_16x16x64_i8(
             r.w[k - i], bd[i], acc[k - kDiagLo], 0, 0, 0);
+#else
+  // round robin over the diagonals: the m-th pair of every diagonal, then
+  // the (m+1)-th -- an accumulator is fed again only after the others
+#pragma unroll
+  for (int m = 0; m < kDigits; ++m)
+#pragma unroll
+    for (int k = kDiagLo; k <= kDiagHi; ++k) {
+      const int i = (k - kDigits + 1 > 0 ? k - kDigits + 1 : 0) + m;
+      if (i <= k && i < kDigits)
+        acc[k - kDiagLo] = __builtin_amdgcn_mfma_i32_16x16x64_i8(
+            r.w[k - i], bd[i], acc[k - kDiagLo], 0, 0, 0);
+    }
+#endif
   v4i R;
 #pragma unroll
   for (int e = 0; e < 4; ++e)
-    R[e] = dig_combine(acc[0][e], acc[1][e], acc[2][e], acc[3][e], acc[4][e], acc[5][e]);
+    R[e] = kDiagLo == 4
+               ? dig_combine(acc[0][e], acc[1][e], acc[2][e], acc[3][e], acc[4][e], acc[5][e])
+               : dig_combine(0, acc[0][e], acc[1][e], acc[2][e], acc[3][e], acc[kNDiag - 1][e]);
   return R;
 }
 
