@@ -235,3 +235,34 @@ def test_int_launches_on_two_streams(ctx, dev):
         ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     for got, w in zip(outs, want):
         assert torch.equal(got.view(torch.int32), w.view(torch.int32))
+
+
+def test_int_range_check_negative_beta_and_bad_grid(ctx, dev):
+    """|Cpix| = (d^2 / r0^2)^(beta / 2) / 2 grows toward the NEAREST grid
+    point when beta < 0: a piercepoint 1e-3 from a grid point makes it
+    ~5e4 > 2^10.9 at beta = -1, so the call keeps the fp64 contraction (the
+    range check takes the nearest point as well as the farthest) and still
+    matches the oracle; non-finite grid coordinates are refused."""
+    from ska_sdp_screen_fitting_amd._lib import SF_EVAL_FAST_SINCOS, ScreenFitError
+    rng = np.random.default_rng(17)
+    D, grid = 48, 32
+    x = np.linspace(-500.0, 500.0, grid)
+    pp = np.stack([rng.uniform(-400, 400, D), rng.uniform(-400, 400, D), np.zeros(D)], 1)
+    pp[7, 0], pp[7, 1] = x[3] + 1e-3, x[5]
+    flags = 1 | SF_EVAL_FAST_SINCOS
+    ctx.set_basis(pp, 100.0, -1.0)
+    ctx.set_grid(x, x)
+    try:
+        assert ctx.eval_contraction(flags) == "f64"
+        coef = rng.normal(0, 1e-7, size=(19, D))
+        o = run(ctx, dev, [coef], 19, grid, True, flags)
+        cpix = okl.cpix_matrix(pp, x, x, beta=-1.0)
+        assert np.abs(cpix).max() > 2 ** 11
+        want = okl.eval_planes(okl.eval_phase_screens(coef, cpix))
+        np.testing.assert_allclose(o.reshape(want.shape), want, rtol=0, atol=2e-6)
+        bad = x.copy()
+        bad[4] = np.nan
+        with pytest.raises(ScreenFitError):
+            ctx.set_grid(bad, x)
+    finally:
+        ctx.set_basis(pp, 100.0, 5.0 / 3.0)
