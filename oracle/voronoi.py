@@ -215,25 +215,27 @@ def label_raster(ra_deg, dec_deg, rad, dec, width, cellsize):
                          crval, crpix, cdelt)
     fmax = sin_world2pix(min(b[2], ra_deg.min() - 0.1), max(b[3], dec_deg.max() + 0.1),
                          crval, crpix, cdelt)
+    tmpl = np.zeros((n, n))
     if len(xy) == 1:
+        # one direction: the field box as the single polygon (:283-293); the
+        # nearest-label fill below then covers the rest of the image
         x0, y0 = float(fmin[0]), float(fmin[1])
         x1, y1 = float(fmax[0]), float(fmax[1])
         tmpl = rasterize([(x0, y0), (x0, y1), (x1, y1), (x1, y0), (x0, y0)], (n, n))
-        return tmpl.astype(np.int32), xy
-    nouter = 64
-    ang = np.array([np.pi / (nouter / 2.0) * i for i in range(nouter)])
-    radius = 2.0 * np.sqrt((float(fmax[0]) - float(fmin[0])) ** 2
-                           + (float(fmax[1]) - float(fmin[1])) ** 2)
-    outer = xy.mean(axis=0) + radius * np.stack([np.cos(ang), np.sin(ang)], 1)
-    vor = Voronoi(np.vstack([xy, outer]))
-    segs = [vor.vertices[r] for r in vor.ridge_vertices if -1 not in r]
-    tmpl = np.zeros((n, n))
-    for ring in geos_polygonize(segs):
-        idx = [k for k in range(len(xy)) if _contains(ring, xy[k, 0], xy[k, 1])]
-        assert len(idx) == 1
-        r = rasterize(ring, (n, n)) * (idx[0] + 1)
-        filled = r > 0
-        tmpl[filled] = r[filled]
+    else:
+        nouter = 64
+        ang = np.array([np.pi / (nouter / 2.0) * i for i in range(nouter)])
+        radius = 2.0 * np.sqrt((float(fmax[0]) - float(fmin[0])) ** 2
+                               + (float(fmax[1]) - float(fmin[1])) ** 2)
+        outer = xy.mean(axis=0) + radius * np.stack([np.cos(ang), np.sin(ang)], 1)
+        vor = Voronoi(np.vstack([xy, outer]))
+        segs = [vor.vertices[r] for r in vor.ridge_vertices if -1 not in r]
+        for ring in geos_polygonize(segs):
+            idx = [k for k in range(len(xy)) if _contains(ring, xy[k, 0], xy[k, 1])]
+            assert len(idx) == 1
+            r = rasterize(ring, (n, n)) * (idx[0] + 1)
+            filled = r > 0
+            tmpl[filled] = r[filled]
     zero = np.where(tmpl == 0)
     if len(zero[0]) > 0:
         nz = np.where(tmpl != 0)

@@ -498,3 +498,54 @@ def test_tess_box_kernel_on_voronoi_rasters(cell, sigma, gain):
     want = _scrub(ov.smooth(ov.gather_planes(lab, ph, ax, ay), sigma))
     scale = np.maximum(1.0, np.abs(want))
     assert np.max(np.abs(res[0] - want) / scale) <= 1e-6
+
+
+def test_single_direction_template():
+    """One direction (make_aterm_images.py:110-112 forces the tessellated
+    screen then, Q14): the raster is the rasterized field box
+    (voronoi_screen.py:241-259) and the griddata fill around it -- every
+    pixel takes label 1; the oracle's restatement agrees."""
+    _, radec = fixture_patches()
+    one = radec[2:3]
+    for cell in (0.2, 0.02602):
+        lab, xy = tessellation_template(one, FIELD["rad"], FIELD["dec"], FIELD["width"], cell)
+        lab_o, _ = ov.label_raster(one[:, 0], one[:, 1], FIELD["rad"], FIELD["dec"],
+                                   FIELD["width"], cell)
+        assert lab.min() == 1 and lab.max() == 1
+        np.testing.assert_array_equal(lab, lab_o)
+        assert xy.shape == (1, 2)
+
+
+@pytest.mark.gpu
+def test_make_aterm_image_one_direction_forces_tessellated(tmp_path):
+    """Q14 end to end: a one-direction solution set asked for a KL screen
+    is written as a tessellated one (the reference cannot fit a KL screen
+    to one direction, make_aterm_images.py:110-112): every pixel of a slot
+    is the referenced phase's cos / sin of that direction (the Gaussian of a
+    constant image is that constant)."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from ska_sdp_screen_fitting_amd import fits as sffits
+    from ska_sdp_screen_fitting_amd.make_aterm_images import make_aterm_image
+    g = load_golden("fixture_kl")
+    k = 2
+    src = {key: g[key] for key in ("times", "freqs", "ant_names", "ant_pos")}
+    src.update(val=g["val"][..., k:k + 1], weight=g["weight"][..., k:k + 1],
+               dir_names=g["dir_names"][k:k + 1], dir_radec=g["dir_radec"][k:k + 1])
+    path = str(tmp_path / "one.npz")
+    np.savez(path, **src)
+    outroot = str(tmp_path / "one")
+    make_aterm_image(path, soltabname="phase000", screen_type="kl", outroot=outroot,
+                     bounds_deg=[124.565, 66.165, 127.895, 62.835],
+                     bounds_mid_deg=[126.23, 64.50], skymodel=SKY,
+                     padding_fraction=0, cellsize_deg=0.2, smooth_deg=0.1, ncpu=0)
+    assert os.path.isfile(outroot + "_template.fits")   # the Voronoi path ran
+    _, cube = sffits.read_cube(outroot + "_0.fits")
+    assert cube.shape == (20, 12, 62, 4, 17, 17)
+    val = np.asarray(g["val"][..., k], np.float64)
+    ph = val - val[:, :, 0:1]                            # reference station 0
+    for p, fn in ((0, np.cos), (1, np.sin), (2, np.cos), (3, np.sin)):
+        want = fn(ph)[..., None, None]
+        np.testing.assert_allclose(cube[:, :, :, p], np.broadcast_to(want, cube[:, :, :, p].shape),
+                                   rtol=0, atol=1e-6)
