@@ -150,3 +150,30 @@ def test_writer_many_members_and_types(tmp_path):
         assert f["grp/u1"].attrs["s"] == b"x"
         np.testing.assert_array_equal(f["grp/u1"].attrs["v"], [0.0, 1.0])
         assert f["scalar"].shape == () and f["scalar"][()] == np.float32(3.5)
+
+
+REF_H5 = "/root/reference/resources/solutions.h5"
+
+
+@pytest.mark.skipif(not os.path.exists(REF_H5),
+                    reason="the reference tree is only present in the build container")
+def test_reference_solutions_h5_reads_as_fixture():
+    """The reference's own resources/solutions.h5 (the file its tests feed
+    make_aterm_image, written by DP3 / PyTables) read by this build's HDF5
+    reader equals the golden fixture the reference itself produced from it
+    (make_golden.py read it with h5py)."""
+    g = load_golden("fixture_kl")
+    ss = H5parm(REF_H5).get_solset("sol000")
+    st = ss.get_soltab("phase000")
+    assert st.get_axes_names() == ["time", "freq", "ant", "dir"]
+    np.testing.assert_array_equal(st.val, g["val"])
+    np.testing.assert_array_equal(st.weight, g["weight"])
+    np.testing.assert_array_equal(st.time, g["times"])
+    np.testing.assert_array_equal(st.freq, g["freqs"])
+    assert list(st.dir) == [str(d) for d in g["dir_names"]]
+    assert list(st.ant) == [str(a) for a in g["ant_names"]]
+    src, ant = ss.get_source(), ss.get_ant()
+    np.testing.assert_array_equal(np.array([src[str(d)] for d in g["dir_names"]]),
+                                  g["dir_radec"])
+    np.testing.assert_array_equal(np.array([ant[str(a)] for a in g["ant_names"]]),
+                                  g["ant_pos"])
