@@ -563,6 +563,88 @@ def dist_block(args, world, record):
             "distinct_devices": len({d.get("uuid") or d.get("pci") for d in devs})}
 
 
+class PowerSampler:
+    """Board power while the timed steps run (read only): the amdgpu hwmon
+    power file of this rank's device in sysfs, sampled every 50 ms by a
+    thread; when the box exposes none, ``amd-smi metric -p --json`` about
+    once a second.  Every KL evaluation runs at the board's power limit
+    ("Energy per output byte"), so the line reports the energy
+    per output byte beside the rate."""
+
+    def __init__(self, pci):
+        import glob
+        self.path, self.samples, self.source = None, [], None
+        dev = f"/sys/bus/pci/devices/{pci}.0" if pci else None
+        for name in ("power1_average", "power1_input"):
+            hits = sorted(glob.glob(f"{dev}/hwmon/hwmon*/{name}")) if dev else []
+            if hits:
+                self.path, self.source = hits[0], hits[0]
+                break
+        if self.path is None and not os.path.exists("/usr/bin/amd-smi") \
+                and not os.path.exists("/opt/rocm/bin/amd-smi"):
+            self.source = None
+        elif self.path is None:
+            self.source = "amd-smi metric -p --json"
+        self._stop = None
+        self._thread = None
+
+    def _read(self):
+        if self.path:
+            with open(self.path) as fh:
+                return int(fh.read().strip()) * 1e-6  # microwatts
+        import subprocess
+        exe = "/opt/rocm/bin/amd-smi" if os.path.exists("/opt/rocm/bin/amd-smi") else "amd-smi"
+        out = subprocess.run([exe, "metric", "-p", "--json"], capture_output=True,
+                             text=True, timeout=10).stdout
+        d = json.loads(out)
+        d = d[0] if isinstance(d, list) else d
+        p = d.get("power", d)
+        v = p.get("socket_power", p.get("average_socket_power"))
+        v = v.get("value") if isinstance(v, dict) else v
+        return float(v)
+
+    def __enter__(self):
+        import threading
+        if self.source is None:
+            return self
+        self._stop = threading.Event()
+
+        def run():
+            period = 0.05 if self.path else 1.0
+            while not self._stop.is_set():
+                try:
+                    w = self._read()
+                    if w > 0:
+                        self.samples.append(w)
+                except (OSError, ValueError, KeyError, TypeError, AttributeError,
+                        json.JSONDecodeError, Exception):
+                    self.source = None
+                    return
+                self._stop.wait(period)
+
+        self._thread = threading.Thread(target=run, daemon=True)
+        self._thread.start()
+        return self
+
+    def __exit__(self, *exc):
+        if self._thread is not None:
+            self._stop.set()
+            self._thread.join(timeout=15)
+        return False
+
+    def summary(self, out_bytes, seconds):
+        """Mean board power and joules per output byte over the timed steps
+        (None when no power source is readable)."""
+        if not self.samples or self.source is None:
+            return None
+        w = float(np.mean(self.samples[1:] if len(self.samples) > 2 else self.samples))
+        return {"board_W_mean": w, "samples": len(self.samples),
+                "source": self.source,
+                "pJ_per_output_byte": w * seconds / out_bytes * 1e12,
+                "what": "mean board power over the timed steps (fit + eval) x their "
+                        "wall time / the bytes of output they stored"}
+
+
 FP64_MFMA_PEAK_TFS = 78.6  # MI355X fp64 matrix peak (AMD spec, dense)
 I8_MFMA_PEAK_TOPS = 5000.0  # MI355X int8 matrix peak (dense; 2x bf16)
 
@@ -702,7 +784,7 @@ def child_leg(extra, what, timeout_s=420):
         "kernel": rf["kernel"], "launch_ms": rf["launch_ms"],
         "bytes_per_launch": rf["bytes_per_launch"], "achieved_GBs": rf["achieved"],
         "frac": rf["frac"], "traffic": rf["traffic"], "mfma": r.get("mfma"),
-        "check": chk, "child_wall_s": wall, "what": what}
+        "power": r.get("power"), "check": chk, "child_wall_s": wall, "what": what}
     if sm:
         out.update(sampled_slots=sm, checksums_match=sm.get("checksums_match"),
                    max_abs_err_vs_fp64=sm["max_abs_err_vs_fp64"], ok=sm["ok"])
@@ -826,19 +908,22 @@ def tess_steps(args, ctx, torch, dev, dist, world, rank, coll_dev, sol, setup,
         dist.barrier()
     torch.cuda.synchronize(dev)
     evs = []
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        step()
-        e1.record(stream)
-        evs.append((e0, e1))
-    torch.cuda.synchronize(dev)
-    if dist.is_initialized():
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    sampler = PowerSampler(args.idents[rank].get("pci"))
+    with sampler:
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            step()
+            e1.record(stream)
+            evs.append((e0, e1))
+        torch.cuda.synchronize(dev)
+        if dist.is_initialized():
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
     local_elapsed = elapsed
+    power = sampler.summary(float(S) * 16 * P * args.steps, local_elapsed)
     tmax = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
     if dist.is_initialized():
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -905,6 +990,7 @@ def tess_steps(args, ctx, torch, dev, dist, world, rank, coll_dev, sol, setup,
                          "traffic": traffic, "kernel": kernel,
                          "bytes_per_launch": bytes_launch,
                          "launch_ms": launch_s * 1e3},
+            "power": power,
             "check": {check_name: unit_err,
                       "slot0_max_ulp_vs_numpy_gather": ulp},
             "dist": dist_info,
@@ -1188,13 +1274,16 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     log(f"timed: {args.steps} steps")
-    t0 = time.perf_counter()
-    ev = run_steps(args.steps)
-    torch.cuda.synchronize(dev)
-    if dist.is_initialized():
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    sampler = PowerSampler(args.idents[rank].get("pci"))
+    with sampler:
+        t0 = time.perf_counter()
+        ev = run_steps(args.steps)
+        torch.cuda.synchronize(dev)
+        if dist.is_initialized():
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
     local_elapsed = elapsed
+    power = sampler.summary(float(S) * 16 * P * args.steps, local_elapsed)
     ctx.set_stream(stream.cuda_stream)
     fit_stats = ctx.fit_stats() if not args.eval_only else {}
     # per-step stage sums; per-launch eval duration for the roofline
@@ -1308,6 +1397,7 @@ def main():
                           "overlap": "fit(c+1) || eval(c), %d time chunks" % n_chunks
                           if n_chunks > 1 else "none"},
             "fit_stats": fit_stats,
+            "power": power,
             "check": {check_name: unit_err, "sampled_slots": sampled},
             "dist": dist_info,
         }
