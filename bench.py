@@ -571,15 +571,16 @@ class PowerSampler:
     ("Energy per output byte"), so the line reports the energy
     per output byte beside the rate."""
 
-    def __init__(self, pci):
+    def __init__(self, pci, path=None):
         import glob
-        self.path, self.samples, self.source = None, [], None
+        self.path, self.samples, self.source = path, [], path
         dev = f"/sys/bus/pci/devices/{pci}.0" if pci else None
         for name in ("power1_average", "power1_input"):
+            if self.path:
+                break
             hits = sorted(glob.glob(f"{dev}/hwmon/hwmon*/{name}")) if dev else []
             if hits:
                 self.path, self.source = hits[0], hits[0]
-                break
         if self.path is None and not os.path.exists("/usr/bin/amd-smi") \
                 and not os.path.exists("/opt/rocm/bin/amd-smi"):
             self.source = None

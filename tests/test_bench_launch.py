@@ -97,3 +97,22 @@ def test_force_dist_one_rank_without_launcher():
     assert len(lines) == 1
     d = json.loads(lines[0])["dist"]
     assert d["backend"] == "gloo" and d["world"] == 1 and len(d["per_rank"]) == 1
+
+
+def test_power_sampler_reads_hwmon_file(tmp_path):
+    """bench.PowerSampler on an hwmon-style file (microwatts): mean board
+    power over the sampled window and joules per output byte."""
+    import time
+    sys.path.insert(0, REPO)
+    import bench
+    f = tmp_path / "power1_average"
+    f.write_text("1250000000\n")                  # 1250 W
+    s = bench.PowerSampler(None, path=str(f))
+    with s:
+        time.sleep(0.4)
+    out = s.summary(out_bytes=6.25e12, seconds=1.0)
+    assert out["board_W_mean"] == pytest.approx(1250.0)
+    assert out["samples"] >= 3
+    assert out["pJ_per_output_byte"] == pytest.approx(200.0)
+    # nothing sampled (never entered): no power object in the line
+    assert bench.PowerSampler(None).summary(1.0, 1.0) is None
