@@ -581,6 +581,10 @@ class PowerSampler:
             hits = sorted(glob.glob(f"{dev}/hwmon/hwmon*/{name}")) if dev else []
             if hits:
                 self.path, self.source = hits[0], hits[0]
+        # the shader clock beside it (amdgpu hwmon freq1 = sclk, in Hz)
+        fq = os.path.join(os.path.dirname(self.path), "freq1_input") if self.path else None
+        self.freq_path = fq if fq and os.path.exists(fq) else None
+        self.clocks = []
         if self.path is None and not os.path.exists("/usr/bin/amd-smi") \
                 and not os.path.exists("/opt/rocm/bin/amd-smi"):
             self.source = None
@@ -617,8 +621,10 @@ class PowerSampler:
                     w = self._read()
                     if w > 0:
                         self.samples.append(w)
-                except (OSError, ValueError, KeyError, TypeError, AttributeError,
-                        json.JSONDecodeError, Exception):
+                    if self.freq_path:
+                        with open(self.freq_path) as fh:
+                            self.clocks.append(int(fh.read().strip()) * 1e-6)
+                except Exception:  # sysfs / amd-smi gone or malformed
                     self.source = None
                     return
                 self._stop.wait(period)
@@ -639,8 +645,10 @@ class PowerSampler:
         if not self.samples or self.source is None:
             return None
         w = float(np.mean(self.samples[1:] if len(self.samples) > 2 else self.samples))
+        clk = self.clocks[1:] if len(self.clocks) > 2 else self.clocks
         return {"board_W_mean": w, "samples": len(self.samples),
                 "source": self.source,
+                "sclk_MHz_mean": float(np.mean(clk)) if clk else None,
                 "pJ_per_output_byte": w * seconds / out_bytes * 1e12,
                 "what": "mean board power over the timed steps (fit + eval) x their "
                         "wall time / the bytes of output they stored"}

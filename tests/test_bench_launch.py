@@ -107,6 +107,7 @@ def test_power_sampler_reads_hwmon_file(tmp_path):
     import bench
     f = tmp_path / "power1_average"
     f.write_text("1250000000\n")                  # 1250 W
+    (tmp_path / "freq1_input").write_text("2100000000\n")  # sclk 2.1 GHz
     s = bench.PowerSampler(None, path=str(f))
     with s:
         time.sleep(0.4)
@@ -114,5 +115,6 @@ def test_power_sampler_reads_hwmon_file(tmp_path):
     assert out["board_W_mean"] == pytest.approx(1250.0)
     assert out["samples"] >= 3
     assert out["pJ_per_output_byte"] == pytest.approx(200.0)
+    assert out["sclk_MHz_mean"] == pytest.approx(2100.0)
     # nothing sampled (never entered): no power object in the line
     assert bench.PowerSampler(None).summary(1.0, 1.0) is None
