@@ -571,6 +571,8 @@ class PowerSampler:
     ("Energy per output byte"), so the line reports the energy
     per output byte beside the rate."""
 
+    MIN_SAMPLES = 20  # ~1 s at the 50 ms sysfs period
+
     def __init__(self, pci, path=None):
         import glob
         self.path, self.samples, self.source = path, [], path
@@ -641,8 +643,11 @@ class PowerSampler:
 
     def summary(self, out_bytes, seconds):
         """Mean board power and joules per output byte over the timed steps
-        (None when no power source is readable)."""
-        if not self.samples or self.source is None:
+        (None when no power source is readable, or when the timed steps
+        took under a second: the hwmon reading averages over a window and
+        lags a short run, e.g. 0.81 kW for a 0.13 s gain run that draws
+        1.37 kW sustained)."""
+        if len(self.samples) < self.MIN_SAMPLES or self.source is None:
             return None
         w = float(np.mean(self.samples[1:] if len(self.samples) > 2 else self.samples))
         clk = self.clocks[1:] if len(self.clocks) > 2 else self.clocks
