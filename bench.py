@@ -83,10 +83,23 @@ def parse():
                          "and takes SIMD and CU time from it when overlapped: "
                          "serial config 4 5.92 M slots/s vs 5.81 pipelined "
                          "(profiles/round2t_schedule_ab.txt)")
+    ap.add_argument("--coef-sets", type=int, default=-1, choices=(-1, 1, 2),
+                    help="coefficient buffers: 2 = the fit of step k+1 writes "
+                         "a second set while step k is evaluated (fit || eval "
+                         "across steps on two streams, as a caller streaming "
+                         "successive solution blocks would run it); the only "
+                         "overlap open to gain screens, whose amplitude fit "
+                         "sees every time at once); -1 (default): 2 for a "
+                         "multi-step gain run (config-3 gain +16 %%), else 1 "
+                         "(config 4: same rate, but the overlapped fit then "
+                         "sits inside the eval's HIP-event window, "
+                         "profiles/round4n_coef_sets_ab.txt)")
     ap.add_argument("--reserve-cus", type=int, default=-1,
                     help="compute units the eval stream leaves to the fit "
-                         "stream (pipelined mode); -1 (default): 16 when "
-                         "D <= 32 (the fit then runs on exactly those), else 0 "
+                         "stream (pipelined mode); -1 (default): 16 with "
+                         "--chunks > 1 and D <= 32 (the fit then runs on "
+                         "exactly those), else 0 (with two coefficient sets "
+                         "and one chunk, 16 reserved CUs cost gain 40 %%) "
                          "(at D = 50 the eval is compute-bound and the fit "
                          "too heavy for 16 CUs: config 5 +8 %%)")
     ap.add_argument("--fit-on-reserved", type=int, default=-1,
@@ -816,7 +829,8 @@ def child_legs():
       (kl_screen.py:411-449), ~45 GB of device buffers;
     * gain_config3: the gain screens (phase + XX / YY amplitude fits, the
       three-contraction eval with 10 **, kl_screen.py:96-125, 319-378) on
-      the config-3 shape, 5 steps;
+      the config-3 shape, 30 steps, two coefficient sets (the fit of step
+      k+1 beside the eval of step k);
     * tess_config3: the tessellated fill (voronoi_screen.py:132-216) on the
       config-3 shape, 10 steps."""
     return {
@@ -825,7 +839,7 @@ def child_legs():
             "one step of config 5's per-GPU shard in a child process "
             "(bench.py --workload config5 --steps 1 --warmup 1)"),
         "gain_config3": child_leg(
-            ["--screen", "gain", "--workload", "config3", "--steps", "5", "--warmup", "1"],
+            ["--screen", "gain", "--workload", "config3", "--steps", "30", "--warmup", "2"],
             "gain screens on the config-3 shape in a child process"),
         "tess_config3": child_leg(
             ["--screen", "tess", "--workload", "config3", "--steps", "10", "--warmup", "2"],
@@ -1159,21 +1173,28 @@ def main():
     # contiguous slice of every array); phase slots are independent, so the
     # fit of one chunk can run while the previous chunk is evaluated
     n_chunks = max(1, min(args.chunks, T))
+    # coefficient sets: step k fits into and evaluates from set k % n_sets
+    n_sets = args.coef_sets if args.coef_sets > 0 else (
+        2 if args.screen == "gain" and args.steps > 1 else 1)
+    coef_sets = [coef] + [torch.empty_like(coef) for _ in range(n_sets - 1)]
+    amp_sets = ([amp["coef"]] + [[torch.empty_like(x) for x in amp["coef"]]
+                                 for _ in range(n_sets - 1)]) if gain else None
+    pipelined = n_chunks > 1 or n_sets > 1
     bounds = [(T * c // n_chunks, T * (c + 1) // n_chunks) for c in range(n_chunks)]
     # the eval saturates HBM without every CU: its stream leaves
     # --reserve-cus compute units (spread over the XCDs) to the fit stream, so
     # the fit of the next chunk is not starved by queued eval workgroups
     fit_stream = stream
     masked_handle = fit_handle = None
-    if n_chunks > 1:
+    if pipelined:
         fit_stream = torch.cuda.Stream(dev, priority=-1 if args.fit_priority else 0)
     # the first fit of a run has the chip to itself (nothing to overlap):
     # it runs on an unrestricted stream even when later fits are confined
     first_fit_stream = fit_stream
-    if n_chunks > 1:
+    if pipelined:
         reserve_cus = args.reserve_cus
         if reserve_cus < 0:
-            reserve_cus = 16 if D <= 32 else 0
+            reserve_cus = 16 if D <= 32 and n_chunks > 1 else 0
         if reserve_cus > 0:
             n_cu = ctx.device_cus()
             step = max(1, n_cu // reserve_cus)
@@ -1201,12 +1222,12 @@ def main():
                                          and args.workload in ("config4", "config5"))
     slot_sums = torch.zeros(S, dtype=torch.int32, device=dev) if checksum else None
 
-    def fit(c, fs):
+    def fit(c, fs, b=0):
         t0, t1 = bounds[c]
         ctx.set_stream(fs.cuda_stream)
         ctx.fit(phase[t0:t1], weight[t0:t1], t1 - t0, F, A, setup["st_order"],
                 niter=2, nsigma=5.0, adjust_order=True, ref_ant=setup["ref_ant"],
-                coef=coef[t0:t1], resid=resid[t0:t1], w_out=w_out[t0:t1],
+                coef=coef_sets[b][t0:t1], resid=resid[t0:t1], w_out=w_out[t0:t1],
                 order_out=order_out[t0:t1], ant_offset=setup["ant_offset"],
                 ref_phase=refph[t0:t1])
         if gain:
@@ -1214,18 +1235,19 @@ def main():
                 ctx.fit(amp["val"][p][t0:t1], amp["w"][p][t0:t1], t1 - t0, F, A,
                         [amp["order"]] * A, screen_type=SF_SCREEN_AMPLITUDE,
                         niter=3, nsigma=5.0, adjust_order=True, ref_ant=-1,
-                        coef=amp["coef"][p][t0:t1], resid=amp["resid"][p][t0:t1],
+                        coef=amp_sets[b][p][t0:t1], resid=amp["resid"][p][t0:t1],
                         w_out=amp["w_out"][p][t0:t1],
                         order_out=amp["orders"][p][t0:t1])
 
-    def evaluate(c):
+    def evaluate(c, b=0):
         t0, t1 = bounds[c]
         ctx.set_stream(stream.cuda_stream)
         n = (t1 - t0) * F * A
+        coef = coef_sets[b]
         cxx = cyy = None
         if gain:
-            cxx = amp["coef"][0][t0:t1].reshape(-1, D)
-            cyy = amp["coef"][1][t0:t1].reshape(-1, D)
+            cxx = amp_sets[b][0][t0:t1].reshape(-1, D)
+            cyy = amp_sets[b][1][t0:t1].reshape(-1, D)
         if checksum:
             ctx.eval_sums(coef[t0:t1].reshape(-1, D), n, out,
                           slot_sums[t0 * F * A:t1 * F * A], ring, coef_xx=cxx,
@@ -1251,15 +1273,16 @@ def main():
             fs = first_fit_stream if i == 0 else fit_stream
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
-            if i >= n_chunks:
-                # coef[chunk c] is rewritten: wait for the previous step's
-                # eval of the same chunk (write-after-read across streams)
-                fs.wait_event(eval_done[i - n_chunks])
+            lag = n_chunks * n_sets
+            if i >= lag:
+                # chunk c of this coefficient set is rewritten: wait for the
+                # eval that last read it (write-after-read across streams)
+                fs.wait_event(eval_done[i - lag])
             if i > 0:
                 fs.wait_event(fit_done[i - 1][1])  # fits share the ctx scratch
             e0.record(fs)
             if not args.eval_only:
-                fit(c, fs)
+                fit(c, fs, k % n_sets)
             e1.record(fs)
             fit_done[i] = (e0, e1)
 
@@ -1269,7 +1292,7 @@ def main():
             e2 = torch.cuda.Event(enable_timing=True)
             e3 = torch.cuda.Event(enable_timing=True)
             e2.record(stream)
-            evaluate(c)
+            evaluate(c, k % n_sets)
             e3.record(stream)
             eval_done[i] = e3
             if i + 1 < len(items):
@@ -1278,8 +1301,9 @@ def main():
         return evs
 
     if args.eval_only:
-        for c in range(n_chunks):
-            fit(c, first_fit_stream)
+        for b in range(n_sets):
+            for c in range(n_chunks):
+                fit(c, first_fit_stream, b)
     log(f"warmup: {args.warmup} steps")
     run_steps(args.warmup)
     torch.cuda.synchronize(dev)
@@ -1392,6 +1416,7 @@ def main():
                 "parallelism": f"ant-shard x{world}",
                 "eval_sincos": "fp64" if args.precise_sincos else "fp32-after-fp64-reduction",
                 "eval_only": bool(args.eval_only),
+                "schedule": {"time_chunks": n_chunks, "coef_sets": n_sets},
             },
             "roofline": {
                 "bound": "hbm",
@@ -1408,8 +1433,9 @@ def main():
             "mfma": mfma_line(eval_kernel_name, S / n_chunks, P, D,
                               t_eval_launch, wkey, 3 if gain else 1, contraction),
             "stages_ms": {"fit": t_fit * 1e3, "eval": t_eval * 1e3,
-                          "overlap": "fit(c+1) || eval(c), %d time chunks" % n_chunks
-                          if n_chunks > 1 else "none"},
+                          "overlap": ("none" if not pipelined else
+                                      "fit(c+1) || eval(c), %d time chunks x %d "
+                                      "coefficient sets" % (n_chunks, n_sets))},
             "fit_stats": fit_stats,
             "power": power,
             "check": {check_name: unit_err, "sampled_slots": sampled},
