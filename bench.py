@@ -90,9 +90,10 @@ def parse():
                          "successive solution blocks would run it); the only "
                          "overlap open to gain screens, whose amplitude fit "
                          "sees every time at once); -1 (default): 2 for a "
-                         "multi-step gain run (config-3 gain +16 %%), else 1 "
-                         "(config 4: same rate, but the overlapped fit then "
-                         "sits inside the eval's HIP-event window, "
+                         "multi-step gain run (config-3 gain +16 %%) or a "
+                         "shard of a multi-GPU run (config 4 / 8: +1.9 %%), "
+                         "else 1 (config 4 on one GPU: same rate, and the "
+                         "fit stays out of the eval's HIP-event window; "
                          "profiles/round4n_coef_sets_ab.txt)")
     ap.add_argument("--reserve-cus", type=int, default=-1,
                     help="compute units the eval stream leaves to the fit "
@@ -1174,8 +1175,9 @@ def main():
     # fit of one chunk can run while the previous chunk is evaluated
     n_chunks = max(1, min(args.chunks, T))
     # coefficient sets: step k fits into and evaluates from set k % n_sets
+    sharded = world > 1 or (args.as_shard_of or 0) > 1
     n_sets = args.coef_sets if args.coef_sets > 0 else (
-        2 if args.screen == "gain" and args.steps > 1 else 1)
+        2 if (args.screen == "gain" or sharded) and args.steps > 1 else 1)
     coef_sets = [coef] + [torch.empty_like(coef) for _ in range(n_sets - 1)]
     amp_sets = ([amp["coef"]] + [[torch.empty_like(x) for x in amp["coef"]]
                                  for _ in range(n_sets - 1)]) if gain else None
