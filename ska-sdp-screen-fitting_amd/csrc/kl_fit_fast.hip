@@ -227,9 +227,46 @@ struct Basis {
   const double* lam;
 };
 
+// The fp64 transcendentals of the fit pass, inlined or called (NI).  Inlined
+// into the two-slots-per-wave pass, their polynomial constants were hoisted
+// out of the slot loop into ~100 VGPRs (235-256 VGPRs: 2 waves per SIMD for
+// a latency-bound kernel); called, that pass fits 128 VGPRs at 4 waves per
+// SIMD (config-4 fit 34 -> 28 ms, gain fits faster still).  The one-slot
+// pass (D > 32) keeps them inlined: called, its config-5 fit got slower.
+// Same functions either way, so the same bits.
+__device__ __noinline__ void nl_sincos(double x, double* s, double* c) { sincos(x, s, c); }
+__device__ __noinline__ double nl_atan2(double y, double x) { return atan2(y, x); }
+__device__ __noinline__ double nl_log10(double x) { return log10(x); }
+__device__ __noinline__ double nl_pow(double x, double y) { return pow(x, y); }
+__device__ __noinline__ double nl_log(double x) { return log(x); }
+__device__ __noinline__ double nl_fmod(double x, double y) { return fmod(x, y); }
+
+template <bool NI>
+struct FitMath {
+  static __device__ __forceinline__ void sin_cos(double x, double* s, double* c) {
+    if constexpr (NI) nl_sincos(x, s, c); else sincos(x, s, c);
+  }
+  static __device__ __forceinline__ double arctan2(double y, double x) {
+    if constexpr (NI) return nl_atan2(y, x); else return atan2(y, x);
+  }
+  static __device__ __forceinline__ double lg10(double x) {
+    if constexpr (NI) return nl_log10(x); else return log10(x);
+  }
+  static __device__ __forceinline__ double power(double x, double y) {
+    if constexpr (NI) return nl_pow(x, y); else return pow(x, y);
+  }
+  static __device__ __forceinline__ double ln(double x) {
+    if constexpr (NI) return nl_log(x); else return log(x);
+  }
+  static __device__ __forceinline__ double mod(double x, double y) {
+    if constexpr (NI) return nl_fmod(x, y); else return fmod(x, y);
+  }
+};
+
+template <bool NI = false>
 __device__ __forceinline__ double model_value(int screen_type, double x) {
   // amplitude screens are log10 values (stationscreen.py:535-548, 576-588)
-  return screen_type == SF_SCREEN_AMPLITUDE ? pow(10.0, x) : x;
+  return screen_type == SF_SCREEN_AMPLITUDE ? FitMath<NI>::power(10.0, x) : x;
 }
 
 // One _fit_screen (stationscreen.py:433-594) in the eigenbasis.  Lanes p < n
@@ -242,6 +279,8 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
                          double& white_d, double& resid_d) {
 #pragma clang fp contract(off)
   using G = Group<SPW>;
+  using M = FitMath<!SLOW && SPW == 2>;
+  constexpr bool NI = !SLOW && SPW == 2;
   const int l = G::lane();
   const int n = B.n;
   double* v0 = L.vec;
@@ -252,11 +291,11 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
   if (l < n) {
     if (screen_type == SF_SCREEN_PHASE) {
       double sn, cn;
-      sincos(phi_p, &sn, &cn);
+      M::sin_cos(phi_p, &sn, &cn);
       rc = w_p * cn;
       rs = w_p * sn;
     } else if (screen_type == SF_SCREEN_AMPLITUDE) {
-      rc = w_p * log10(phi_p);
+      rc = w_p * M::lg10(phi_p);
     } else {
       rc = w_p * phi_p;
     }
@@ -343,7 +382,7 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
       cre += u * v0[k];
       cim += u * v1[k];
     }
-    screen = (screen_type == SF_SCREEN_PHASE) ? atan2(cim, cre) : cre;
+    screen = (screen_type == SF_SCREEN_PHASE) ? M::arctan2(cim, cre) : cre;
   }
   lds_sync();
   if (l < n) v2[l] = screen;
@@ -369,7 +408,7 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
   lds_sync();
   if (B.full) {
     white_d = white;
-    resid_d = phi_d - model_value(screen_type, cw);
+    resid_d = phi_d - model_value<NI>(screen_type, cw);
     return;
   }
   // flagged directions (stationscreen.py:565-582): screen from the subset's
@@ -413,15 +452,16 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
     for (int r = 0; r < D; ++r) wa += L.U[l * ld + r] * v0[r];
   lds_sync();
   white_d = wa;
-  resid_d = phi_d - model_value(screen_type, sall);
+  resid_d = phi_d - model_value<NI>(screen_type, sall);
 }
 
 // residual as the outlier test / chi^2 see it (stationscreen.py:660-668,
 // 733-746): phase & tec use the residual, amplitude the log10 ratio
+template <bool NI = false>
 __device__ __forceinline__ double screen_diff(int screen_type, double val,
                                               double resid) {
   if (screen_type == SF_SCREEN_AMPLITUDE)
-    return log10(val) - log10(fabs(val - resid));
+    return FitMath<NI>::lg10(val) - FitMath<NI>::lg10(fabs(val - resid));
   return resid;
 }
 
@@ -431,10 +471,10 @@ __device__ __forceinline__ double screen_diff(int screen_type, double val,
 // per-slot LDS is the 3 KiB of vectors and 2.7x (D = 20) to 4x (D = 50) more
 // waves fit on a CU; the kernel is latency-bound, so occupancy is its speed.
 #ifndef SF_FIT_MINW
-#define SF_FIT_MINW 1  // waves per SIMD the register budget must admit
+#define SF_FIT_MINW 4  // waves per SIMD of the two-slot fast pass (128 VGPRs)
 #endif
 template <bool SLOW, int SPW, bool LEAN>
-__global__ __launch_bounds__(256, SF_FIT_MINW) void kl_fit_pass_kernel(
+__global__ __launch_bounds__(256, (!SLOW && SPW == 2) ? SF_FIT_MINW : 1) void kl_fit_pass_kernel(
     int it, int niter, int64_t S, int F, int A, int D,
     const double* __restrict__ phase, const double* __restrict__ refph,
     int ref_sub, const double* __restrict__ g_u, const double* __restrict__ g_c,
@@ -449,6 +489,8 @@ __global__ __launch_bounds__(256, SF_FIT_MINW) void kl_fit_pass_kernel(
   extern __shared__ double smem[];
   const int ld = ldo(D);
   using G = Group<SPW>;
+  using M = FitMath<!SLOW && SPW == 2>;
+  constexpr bool NI = !SLOW && SPW == 2;
   const int nwaves = blockDim.x / 64;
   const int nslots = nwaves * SPW;                  // slots in flight per WG
   const int wv = (threadIdx.x / 64) * SPW + G::index();  // slot of the WG
@@ -585,7 +627,7 @@ __global__ __launch_bounds__(256, SF_FIT_MINW) void kl_fit_pass_kernel(
           double redchi2;
           if (screen_type == SF_SCREEN_PHASE) {
             double sn = 0.0, cn = 0.0;
-            if (unfl) sincos(resid_d, &sn, &cn);
+            if (unfl) M::sin_cos(resid_d, &sn, &cn);
             const double ww = unfl ? w_d : 0.0;
             const double sw = G::sum(ww);
             const double m1 = G::sum(sn * sn * ww) / sw;
@@ -595,7 +637,7 @@ __global__ __launch_bounds__(256, SF_FIT_MINW) void kl_fit_pass_kernel(
             // np.sum(square(diff) * w) over all directions
             double t = 0.0;
             if (d < D) {
-              const double sd = screen_diff(screen_type, phi_d, resid_d);
+              const double sd = screen_diff<NI>(screen_type, phi_d, resid_d);
               t = (sd * sd) * w_d;
             }
             redchi2 = G::sum(t) / (n_unfl - order);
@@ -605,7 +647,7 @@ __global__ __launch_bounds__(256, SF_FIT_MINW) void kl_fit_pass_kernel(
             if (redchi2 < 1.0 && prev_redchi2 > redchi2) sign = -sign;
           }
           prev_redchi2 = redchi2;
-          const double order_factor = pow((double)n_unfl - order, 0.2);
+          const double order_factor = M::power((double)n_unfl - order, 0.2);
           double target = order - sign * order_factor * (1.0 - redchi2);
           target = fmax(station_order, target);
           target = fmin(rint(target), (double)(n_unfl - 1));
@@ -629,16 +671,16 @@ __global__ __launch_bounds__(256, SF_FIT_MINW) void kl_fit_pass_kernel(
     if (it + 1 < niter && screen_type == SF_SCREEN_PHASE) {
       const bool live = d < D;
       if (G::any(live && w_d > 0.0)) {
-        double r = fmod(resid_d, 2.0 * M_PI);
+        double r = M::mod(resid_d, 2.0 * M_PI);
         if (r < -M_PI) r += 2.0 * M_PI;
         if (r > M_PI) r -= 2.0 * M_PI;
         const bool inc = live && (w_d != 0.0) && !isnan(r);
         double sn = 0.0, cn = 0.0;
-        if (inc) sincos(r, &sn, &cn);
+        if (inc) M::sin_cos(r, &sn, &cn);
         const double cnt = G::sum(inc ? 1.0 : 0.0);
         const double ms = G::sum(sn) / cnt;
         const double mc = G::sum(cn) / cnt;
-        const double stdv = sqrt(-2.0 * log(hypot(ms, mc)));
+        const double stdv = sqrt(-2.0 * M::ln(hypot(ms, mc)));
         const bool outl = live && (fabs(r) > nsigma * stdv);
         if (outl) w_d = 0.0;
         if (G::any(outl)) {
