@@ -149,15 +149,21 @@ __global__ __launch_bounds__(256) void kl_assign_kernel(
 
 // 3. subset bases of the masks numbered [counters[1], counters[0]):
 //    C_sub = C[idx][:, idx] -> Jacobi -> U_sub sorted by |lambda| desc.
+//    A pool mask leaves at least one direction out (the full mask is the
+//    global basis, kl_classify_kernel), so the LDS matrices are sized for
+//    D - 1 rows: at D = 50 a wave's 40,720 bytes let 4 waves share a CU's
+//    160 KiB (43,104 bytes, sized for D, let 3).
+__host__ __device__ inline int subset_ld(int D) { return ldo(D > 1 ? D - 1 : 1); }
+__host__ __device__ inline int subset_rows(int D) { return D > 1 ? D - 1 : 1; }
 __global__ __launch_bounds__(64) void kl_subset_eig_kernel(
     const double* __restrict__ g_c, int D,
     const unsigned long long* __restrict__ pool_mask, int pool_cap,
-    const int* __restrict__ counters, double* __restrict__ pool) {
+    int* __restrict__ counters, double* __restrict__ pool) {
   extern __shared__ double smem[];
-  const int ld = ldo(D);
+  const int ld = subset_ld(D);
   double* a = smem;
-  double* v = a + D * ld;
-  double2* cs = reinterpret_cast<double2*>(v + D * ld);
+  double* v = a + subset_rows(D) * ld;
+  double2* cs = reinterpret_cast<double2*>(v + subset_rows(D) * ld);
   int2* pr = reinterpret_cast<int2*>(cs + 64);  // 64 int2 + 64 int
   int* perm = reinterpret_cast<int*>(pr + 96);
   int* idx = perm + 64;
@@ -168,6 +174,10 @@ __global__ __launch_bounds__(64) void kl_subset_eig_kernel(
     const unsigned long long m = pool_mask[id];
     const bool in = (l < D) && ((m >> l) & 1ull);
     const int n = __popcll(m);
+    if (n >= D) {  // cannot happen (full masks never enter the pool): flag it
+      if (l == 0) atomicOr(counters + 3, 2);
+      continue;
+    }
     if (in) {
       const int p = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                               __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
@@ -865,7 +875,7 @@ static int number_and_decompose(sf_ctx* ctx, int* n_slow, int* n_nonuniform) {
   const int n_new = cnt[0] - cnt[1];
   if (n_new > 0) {
     const int D = ctx->D;
-    const size_t shm = (size_t)2 * D * ldo(D) * sizeof(double) +
+    const size_t shm = (size_t)2 * subset_rows(D) * subset_ld(D) * sizeof(double) +
                        64 * sizeof(double2) + 96 * sizeof(int2) +
                        128 * sizeof(int);
     if (shm > 64 * 1024)
