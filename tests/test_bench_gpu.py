@@ -1,0 +1,42 @@
+"""bench.py's step schedules on the GPU: the two-coefficient-set schedule
+(the fit of step k+1 on a second stream beside the eval of step k) for phase
+and gain screens, on the small ``tiny`` workload, checked by the bench's own
+sampled-slot comparison against an fp64 restatement and the plane
+invariants.  Each run is one child process of bench.py."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(*args):
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--workload", "tiny",
+           "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-side-legs",
+           "--no-fits", "--no-child-legs", *args]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("screen", ["phase", "gain"])
+def test_two_coefficient_sets_schedule(screen):
+    extra = ["--screen", "gain"] if screen == "gain" else []
+    one = _bench("--coef-sets", "1", *extra)
+    two = _bench("--coef-sets", "2", *extra)
+    assert one["config"]["schedule"]["coef_sets"] == 1
+    assert two["config"]["schedule"]["coef_sets"] == 2
+    assert "2 coefficient sets" in two["stages_ms"]["overlap"]
+    for line in (one, two):
+        s = line["check"]["sampled_slots"]
+        assert s["ok"], s
+        assert line["value"] > 0
+    # the default picks two sets for multi-step gain runs, one for phase
+    default = _bench(*extra)
+    assert default["config"]["schedule"]["coef_sets"] == (2 if screen == "gain" else 1)
