@@ -209,7 +209,8 @@ __global__ __launch_bounds__(64) void kl_subset_eig_kernel(
 // ---------------------------------------------------------------------------
 struct FastLds {
   const double* U;    // [D][ld] full basis, columns sorted
-  const double* C;    // [D][ld]
+  const double* C;    // [D][cld]: LDS, or global for the one-slot pass
+  int cld;            // row stride of C
   const double* lam;  // [64]
   double* Vs;         // per wave: subset basis [D][ld]
   double* lams;       // per wave [64]
@@ -220,8 +221,10 @@ struct FastLds {
   int2* pr;           // per wave [96]   (SLOW: Jacobi scratch)
 };
 
-__host__ __device__ inline size_t fast_shared_bytes(int D) {
-  return (size_t)(2 * D * ldo(D) + 64) * sizeof(double);
+// U (and C, except in the one-slot pass, which reads C from L2: at D = 50
+// that halves the workgroup's shared LDS so 4 waves per SIMD fit) + lambda
+__host__ __device__ inline size_t fast_shared_bytes(int D, bool c_global) {
+  return (size_t)((c_global ? 1 : 2) * D * ldo(D) + 64) * sizeof(double);
 }
 __host__ __device__ inline size_t fast_wave_bytes(int D, bool slow, bool lean = false) {
   if (lean) return (size_t)6 * 64 * sizeof(double);  // the vectors only
@@ -242,8 +245,9 @@ struct Basis {
 // out of the slot loop into ~100 VGPRs (235-256 VGPRs: 2 waves per SIMD for
 // a latency-bound kernel); called, that pass fits 128 VGPRs at 4 waves per
 // SIMD (config-4 fit 34 -> 28 ms, gain fits faster still).  The one-slot
-// pass (D > 32) keeps them inlined: called, its config-5 fit got slower.
-// Same functions either way, so the same bits.
+// pass (D > 32) calls them too, with C read from L2 so that its LDS admits
+// the same 4 waves per SIMD (calls alone, LDS-capped at 3, were slower).
+// The SLOW class keeps them inlined.  Same functions either way, same bits.
 __device__ __noinline__ void nl_sincos(double x, double* s, double* c) { sincos(x, s, c); }
 __device__ __noinline__ double nl_atan2(double y, double x) { return atan2(y, x); }
 __device__ __noinline__ double nl_log10(double x) { return log10(x); }
@@ -289,8 +293,8 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
                          double& white_d, double& resid_d) {
 #pragma clang fp contract(off)
   using G = Group<SPW>;
-  using M = FitMath<!SLOW && SPW == 2>;
-  constexpr bool NI = !SLOW && SPW == 2;
+  using M = FitMath<!SLOW>;
+  constexpr bool NI = !SLOW;
   const int l = G::lane();
   const int n = B.n;
   double* v0 = L.vec;
@@ -441,7 +445,7 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
       int p = 0;
       while (mm) {
         const int q = __builtin_ctzll(mm);
-        sall += L.C[l * ld + q] * v1[p];
+        sall += L.C[l * L.cld + q] * v1[p];
         mm &= mm - 1;
         ++p;
       }
@@ -484,7 +488,7 @@ __device__ __forceinline__ double screen_diff(int screen_type, double val,
 #define SF_FIT_MINW 4  // waves per SIMD of the two-slot fast pass (128 VGPRs)
 #endif
 template <bool SLOW, int SPW, bool LEAN>
-__global__ __launch_bounds__(256, (!SLOW && SPW == 2) ? SF_FIT_MINW : 1) void kl_fit_pass_kernel(
+__global__ __launch_bounds__(256, SLOW ? 1 : SF_FIT_MINW) void kl_fit_pass_kernel(
     int it, int niter, int64_t S, int F, int A, int D,
     const double* __restrict__ phase, const double* __restrict__ refph,
     int ref_sub, const double* __restrict__ g_u, const double* __restrict__ g_c,
@@ -499,25 +503,27 @@ __global__ __launch_bounds__(256, (!SLOW && SPW == 2) ? SF_FIT_MINW : 1) void kl
   extern __shared__ double smem[];
   const int ld = ldo(D);
   using G = Group<SPW>;
-  using M = FitMath<!SLOW && SPW == 2>;
-  constexpr bool NI = !SLOW && SPW == 2;
+  using M = FitMath<!SLOW>;
+  constexpr bool NI = !SLOW;
+  constexpr bool CG = SPW == 1;  // C read from global (L2), not LDS
   const int nwaves = blockDim.x / 64;
   const int nslots = nwaves * SPW;                  // slots in flight per WG
   const int wv = (threadIdx.x / 64) * SPW + G::index();  // slot of the WG
   const int d = G::lane();
   double* sU = smem;
-  double* sC = sU + D * ld;
-  double* sl = sC + D * ld;
+  double* sC = CG ? nullptr : sU + D * ld;
+  double* sl = sU + (CG ? 1 : 2) * D * ld;
   for (int e = threadIdx.x; e < D * D; e += blockDim.x) {
     const int r = e / D, c = e % D;
     sU[r * ld + c] = g_u[e];
-    sC[r * ld + c] = g_c[e];
+    if (!CG) sC[r * ld + c] = g_c[e];
   }
   for (int e = threadIdx.x; e < 64; e += blockDim.x) sl[e] = e < D ? g_eig[e] : 0.0;
   __syncthreads();
   FastLds L;
   L.U = sU;
-  L.C = sC;
+  L.C = CG ? g_c : sC;
+  L.cld = CG ? D : ld;
   L.lam = sl;
   double* wb = sl + 64 + (size_t)wv * (fast_wave_bytes(D, SLOW, LEAN) / sizeof(double));
   if (LEAN) {
@@ -897,7 +903,7 @@ static int launch_pass_spw(sf_ctx* ctx, int it, const sf_fit_params* p,
                            const double* phase, double* coef, double* resid,
                            float* w_out, int32_t* order_out) {
   const int D = ctx->D;
-  const size_t shared = fast_shared_bytes(D);
+  const size_t shared = fast_shared_bytes(D, SPW == 1);
   const size_t slot = fast_wave_bytes(D, SLOW, LEAN);  // per-slot LDS scratch
   // waves per workgroup (<= 4): the most resident waves per CU under the
   // 160 KiB LDS of a gfx950 CU (the per-slot subset basis is D^2 doubles,
