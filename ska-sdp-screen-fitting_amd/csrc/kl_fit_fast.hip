@@ -155,7 +155,7 @@ __global__ __launch_bounds__(256) void kl_assign_kernel(
 //    160 KiB (43,104 bytes, sized for D, let 3).
 __host__ __device__ inline int subset_ld(int D) { return ldo(D > 1 ? D - 1 : 1); }
 __host__ __device__ inline int subset_rows(int D) { return D > 1 ? D - 1 : 1; }
-__global__ __launch_bounds__(64) void kl_subset_eig_kernel(
+__global__ __launch_bounds__(128) void kl_subset_eig_kernel(
     const double* __restrict__ g_c, int D,
     const unsigned long long* __restrict__ pool_mask, int pool_cap,
     int* __restrict__ counters, double* __restrict__ pool) {
@@ -170,34 +170,36 @@ __global__ __launch_bounds__(64) void kl_subset_eig_kernel(
   const int first = counters[1];
   const int last = min(counters[0], pool_cap);
   const int l = lane();
+  const bool w0 = threadIdx.x < 64;  // two waves per mask (wg2_jacobi)
   for (int id = first + blockIdx.x; id < last; id += gridDim.x) {
     const unsigned long long m = pool_mask[id];
     const bool in = (l < D) && ((m >> l) & 1ull);
     const int n = __popcll(m);
     if (n >= D) {  // cannot happen (full masks never enter the pool): flag it
-      if (l == 0) atomicOr(counters + 3, 2);
+      if (threadIdx.x == 0) atomicOr(counters + 3, 2);
       continue;
     }
-    if (in) {
+    if (w0 && in) {
       const int p = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                               __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
       idx[p] = l;
     }
-    lds_sync();
-    if (l < n) {
+    __syncthreads();
+    if (w0 && l < n) {
       const int r = idx[l];
       for (int q = 0; q < n; ++q) a[l * ld + q] = g_c[r * D + idx[q]];
     }
-    lds_sync();
-    wave_jacobi(a, v, cs, pr, n, ld, 40);
-    wave_eig_order(a, n, ld, perm);
+    __syncthreads();
+    wg2_jacobi(a, v, cs, pr, n, ld, 40);
+    __syncthreads();
+    if (w0) wave_eig_order(a, n, ld, perm);
     double* e = pool + (size_t)id * (D * D + D);
-    if (l < n) {
+    if (w0 && l < n) {
       for (int r = 0; r < n; ++r) e[l * D + r] = v[l * ld + perm[r]];
       const int pr = perm[l];
       e[D * D + l] = a[pr * ld + pr];
     }
-    lds_sync();
+    __syncthreads();
   }
 }
 
@@ -889,7 +891,7 @@ static int number_and_decompose(sf_ctx* ctx, int* n_slow, int* n_nonuniform) {
           reinterpret_cast<const void*>(&kl_subset_eig_kernel),
           hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
     const int blocks = n_new < 8192 ? n_new : 8192;
-    hipLaunchKernelGGL(kl_subset_eig_kernel, dim3(blocks), dim3(64), shm,
+    hipLaunchKernelGGL(kl_subset_eig_kernel, dim3(blocks), dim3(128), shm,
                        ctx->stream, ctx->d_c, D, ctx->d_pool_mask,
                        (int)ctx->pool_cap, ctx->d_counters, ctx->d_pool);
     SF_HIP(hipGetLastError());

@@ -218,6 +218,131 @@ __device__ inline int wave_jacobi(double* a, double* v, double2* cs, int2* pr,
   return sweep;
 }
 
+// wave_jacobi on a workgroup of two waves (128 threads): the same rounds,
+// rotations and per-element arithmetic -- so the same bits -- with each
+// round's column pairs split between the waves (wave 0 the first half, wave
+// 1 the rest; lane i of both owns row i) and a workgroup barrier where the
+// one-wave version relies on wave order: after wave 0 computes the round's
+// rotations, and at the end of every round.  The waves write disjoint
+// columns within a round, and every read of a round precedes its barrier.
+// With one wave per SIMD the one-wave solve sat exposed to every LDS and
+// fp64 latency; two waves halve each round's update work and overlap.
+__device__ inline int wg2_jacobi(double* a, double* v, double2* cs, int2* pr,
+                                 int n, int ld, int max_sweeps) {
+#pragma clang fp contract(off)
+  const int i = lane();
+  const int w = threadIdx.x >> 6;
+  const bool own = i < n;
+  const int m = n + (n & 1);
+  const int npairs = m / 2;
+  const int half = (npairs + 1) / 2;
+  const int kb = w ? half : 0;
+  const int ke = w ? npairs : half;
+  int* part = reinterpret_cast<int*>(pr + 64);
+  for (int j = w; j < n; j += 2)
+    if (own) v[i * ld + j] = (i == j) ? 1.0 : 0.0;
+  __syncthreads();
+  int sweep = 0;
+  for (; sweep < max_sweeps; ++sweep) {
+    // both waves reduce the same rows in the same order: the same decision
+    double off = 0.0, dia = 0.0;
+    if (own) {
+      for (int j = 0; j < n; ++j) {
+        const double x = a[i * ld + j];
+        if (j == i) dia += x * x; else off += x * x;
+      }
+    }
+    off = wave_sum(off);
+    dia = wave_sum(dia);
+    if (!(off > 1e-26 * (off + dia))) break;
+    for (int r = 0; r < m - 1; ++r) {
+      if (w == 0 && i < npairs) {
+        int p, q;
+        if (i == 0) {
+          p = r;
+          q = m - 1;
+        } else {
+          p = r + i;
+          if (p >= m - 1) p -= m - 1;
+          q = r - i;
+          if (q < 0) q += m - 1;
+        }
+        if (q >= n) q = p;
+        if (p >= n) p = q;
+        if (p > q) { const int t = p; p = q; q = t; }
+        double c = 1.0, s = 0.0;
+        const double apq = a[p * ld + q];
+        if (p != q && apq != 0.0) {
+          const double app = a[p * ld + p];
+          const double aqq = a[q * ld + q];
+          const double tau = (aqq - app) / (2.0 * apq);
+          double t;
+          if (fabs(tau) > 1e150) {
+            t = 0.5 / tau;
+          } else {
+            t = 1.0 / (fabs(tau) + sqrt(1.0 + tau * tau));
+            if (tau < 0.0) t = -t;
+          }
+          c = 1.0 / sqrt(1.0 + t * t);
+          s = t * c;
+        }
+        pr[i] = make_int2(p, q);
+        cs[p] = make_double2(c, -s);
+        part[p] = q;
+        if (q != p) {
+          cs[q] = make_double2(c, s);
+          part[q] = p;
+        }
+      }
+      __syncthreads();
+      const double2 ri = own ? cs[i] : make_double2(1.0, 0.0);
+      const int pir = own ? part[i] : 0;
+      constexpr int CH = 4;  // column pairs per chunk
+      for (int k0 = kb; k0 < ke; k0 += CH) {
+        double na[CH], nb[CH], nv[CH], nw[CH];
+        int jj[CH], qq[CH];
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+          const int k = min(k0 + u, ke - 1);
+          const int2 jq = pr[k];
+          const int j = jq.x, pj = jq.y;
+          jj[u] = j;
+          qq[u] = pj;
+          const double2 rj = cs[j];
+          const double2 rq = cs[pj];
+          const double aij = a[i * ld + j];
+          const double aiq = a[i * ld + pj];
+          const double apj = a[pir * ld + j];
+          const double apq = a[pir * ld + pj];
+          const double vij = v[i * ld + j];
+          const double viq = v[i * ld + pj];
+          const double r_j = ri.x * aij + ri.y * apj;
+          const double r_q = ri.x * aiq + ri.y * apq;
+          na[u] = rj.x * r_j + rj.y * r_q;
+          nb[u] = rq.x * r_q + rq.y * r_j;
+          nv[u] = rj.x * vij + rj.y * viq;
+          nw[u] = rq.x * viq + rq.y * vij;
+        }
+        lds_sync();
+        if (own) {
+#pragma unroll
+          for (int u = 0; u < CH; ++u) {
+            a[i * ld + jj[u]] = na[u];
+            v[i * ld + jj[u]] = nv[u];
+            if (qq[u] != jj[u]) {
+              a[i * ld + qq[u]] = nb[u];
+              v[i * ld + qq[u]] = nw[u];
+            }
+          }
+        }
+        lds_sync();
+      }
+      __syncthreads();
+    }
+  }
+  return sweep;
+}
+
 // Rank of lane i's eigenvalue by descending |lambda| (ties by index), i.e.
 // the column order of U from svd() of a symmetric matrix.  Writes
 // perm[rank] = i for i < n.
