@@ -155,7 +155,10 @@ __global__ __launch_bounds__(256) void kl_assign_kernel(
 //    160 KiB (43,104 bytes, sized for D, let 3).
 __host__ __device__ inline int subset_ld(int D) { return ldo(D > 1 ? D - 1 : 1); }
 __host__ __device__ inline int subset_rows(int D) { return D > 1 ? D - 1 : 1; }
-__global__ __launch_bounds__(128) void kl_subset_eig_kernel(
+#ifndef SF_EIG_WAVES
+#define SF_EIG_WAVES 2  // waves per mask of the subset Jacobi (wg_jacobi)
+#endif
+__global__ __launch_bounds__(64 * SF_EIG_WAVES) void kl_subset_eig_kernel(
     const double* __restrict__ g_c, int D,
     const unsigned long long* __restrict__ pool_mask, int pool_cap,
     int* __restrict__ counters, double* __restrict__ pool) {
@@ -170,7 +173,7 @@ __global__ __launch_bounds__(128) void kl_subset_eig_kernel(
   const int first = counters[1];
   const int last = min(counters[0], pool_cap);
   const int l = lane();
-  const bool w0 = threadIdx.x < 64;  // two waves per mask (wg2_jacobi)
+  const bool w0 = threadIdx.x < 64;  // SF_EIG_WAVES waves per mask
   for (int id = first + blockIdx.x; id < last; id += gridDim.x) {
     const unsigned long long m = pool_mask[id];
     const bool in = (l < D) && ((m >> l) & 1ull);
@@ -190,7 +193,7 @@ __global__ __launch_bounds__(128) void kl_subset_eig_kernel(
       for (int q = 0; q < n; ++q) a[l * ld + q] = g_c[r * D + idx[q]];
     }
     __syncthreads();
-    wg2_jacobi(a, v, cs, pr, n, ld, 40);
+    wg_jacobi<SF_EIG_WAVES>(a, v, cs, pr, n, ld, 40);
     __syncthreads();
     if (w0) wave_eig_order(a, n, ld, perm);
     double* e = pool + (size_t)id * (D * D + D);
@@ -891,7 +894,7 @@ static int number_and_decompose(sf_ctx* ctx, int* n_slow, int* n_nonuniform) {
           reinterpret_cast<const void*>(&kl_subset_eig_kernel),
           hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
     const int blocks = n_new < 8192 ? n_new : 8192;
-    hipLaunchKernelGGL(kl_subset_eig_kernel, dim3(blocks), dim3(128), shm,
+    hipLaunchKernelGGL(kl_subset_eig_kernel, dim3(blocks), dim3(64 * SF_EIG_WAVES), shm,
                        ctx->stream, ctx->d_c, D, ctx->d_pool_mask,
                        (int)ctx->pool_cap, ctx->d_counters, ctx->d_pool);
     SF_HIP(hipGetLastError());

@@ -218,28 +218,29 @@ __device__ inline int wave_jacobi(double* a, double* v, double2* cs, int2* pr,
   return sweep;
 }
 
-// wave_jacobi on a workgroup of two waves (128 threads): the same rounds,
+// wave_jacobi on a workgroup of NW waves (64 NW threads): the same rounds,
 // rotations and per-element arithmetic -- so the same bits -- with each
-// round's column pairs split between the waves (wave 0 the first half, wave
-// 1 the rest; lane i of both owns row i) and a workgroup barrier where the
+// round's column pairs split between the waves (consecutive shares; lane i
+// of every wave owns row i) and a workgroup barrier where the
 // one-wave version relies on wave order: after wave 0 computes the round's
 // rotations, and at the end of every round.  The waves write disjoint
 // columns within a round, and every read of a round precedes its barrier.
 // With one wave per SIMD the one-wave solve sat exposed to every LDS and
-// fp64 latency; two waves halve each round's update work and overlap.
-__device__ inline int wg2_jacobi(double* a, double* v, double2* cs, int2* pr,
-                                 int n, int ld, int max_sweeps) {
+// fp64 latency; more waves split each round's update work and overlap.
+template <int NW = 2>
+__device__ inline int wg_jacobi(double* a, double* v, double2* cs, int2* pr,
+                                int n, int ld, int max_sweeps) {
 #pragma clang fp contract(off)
   const int i = lane();
   const int w = threadIdx.x >> 6;
   const bool own = i < n;
   const int m = n + (n & 1);
   const int npairs = m / 2;
-  const int half = (npairs + 1) / 2;
-  const int kb = w ? half : 0;
-  const int ke = w ? npairs : half;
+  const int share = (npairs + NW - 1) / NW;  // column pairs per wave
+  const int kb = min(w * share, npairs);
+  const int ke = min(kb + share, npairs);
   int* part = reinterpret_cast<int*>(pr + 64);
-  for (int j = w; j < n; j += 2)
+  for (int j = w; j < n; j += NW)
     if (own) v[i * ld + j] = (i == j) ? 1.0 : 0.0;
   __syncthreads();
   int sweep = 0;
