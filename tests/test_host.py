@@ -109,3 +109,22 @@ def test_fits_card_format():
     assert sffits.card("CTYPE1", "RA---SIN") == "CTYPE1  = 'RA---SIN'".ljust(80)
     assert sffits.card("SIMPLE", True) == "SIMPLE  =                    T".ljust(80)
     assert sffits.card("CUNIT3", "") == "CUNIT3  = '        '".ljust(80)
+
+
+def test_wg_jacobi_pair_shares_cover_every_pair_once():
+    """wg_jacobi<NW> (sf_wave.h) splits each round's column pairs into
+    consecutive shares, one per wave: for every subset size (1..63
+    directions) and wave count, every pair belongs to exactly one wave, so
+    each column of a round is written once (the same rotations as the
+    one-wave solve)."""
+    for nw in (1, 2, 3, 4):
+        for n in range(1, 64):
+            m = n + (n & 1)
+            npairs = m // 2
+            share = (npairs + nw - 1) // nw
+            owned = []
+            for w in range(nw):
+                kb = min(w * share, npairs)
+                ke = min(kb + share, npairs)
+                owned.extend(range(kb, ke))
+            assert sorted(owned) == list(range(npairs)), (nw, n)
