@@ -156,7 +156,7 @@ __global__ __launch_bounds__(256) void kl_assign_kernel(
 __host__ __device__ inline int subset_ld(int D) { return ldo(D > 1 ? D - 1 : 1); }
 __host__ __device__ inline int subset_rows(int D) { return D > 1 ? D - 1 : 1; }
 #ifndef SF_EIG_WAVES
-#define SF_EIG_WAVES 2  // waves per mask of the subset Jacobi (wg_jacobi)
+#define SF_EIG_WAVES 3  // waves per mask of the subset Jacobi (wg_jacobi)
 #endif
 __global__ __launch_bounds__(64 * SF_EIG_WAVES) void kl_subset_eig_kernel(
     const double* __restrict__ g_c, int D,
