@@ -87,14 +87,13 @@ def parse():
                     help="coefficient buffers: 2 = the fit of step k+1 writes "
                          "a second set while step k is evaluated (fit || eval "
                          "across steps on two streams, as a caller streaming "
-                         "successive solution blocks would run it); the only "
+                         "successive solution blocks would run it; the only "
                          "overlap open to gain screens, whose amplitude fit "
                          "sees every time at once); -1 (default): 2 for a "
-                         "multi-step gain run (config-3 gain +16 %%) or a "
-                         "shard of a multi-GPU run (config 4 / 8: +1.9 %%), "
-                         "else 1 (config 4 on one GPU: same rate, and the "
-                         "fit stays out of the eval's HIP-event window; "
-                         "profiles/round4n_coef_sets_ab.txt)")
+                         "multi-step gain run (config-3 gain +16 %%), else 1 "
+                         "-- at every --gpus N, so the driver's 1 -> 8 curve "
+                         "divides like by like (config 4: one or two sets "
+                         "measured within 1.9 %%, profiles/round4n_coef_sets_ab.txt)")
     ap.add_argument("--reserve-cus", type=int, default=-1,
                     help="compute units the eval stream leaves to the fit "
                          "stream (pipelined mode); -1 (default): 16 with "
@@ -146,6 +145,10 @@ def parse():
                          "then the three-contraction gain evaluation; "
                          "tess: the tessellated (Voronoi) fill of every slot "
                          "(voronoi_screen.py:132-216, sf_tess_fill), no fit")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="skip the parity checks against the reference's golden "
+                         "outputs (tools/bench_parity.py; on by default, the "
+                         "line exits 3 when one fails)")
     ap.add_argument("--eval-only", action="store_true",
                     help="time only sf_kl_eval (profiling)")
     ap.add_argument("--as-shard-of", type=int, default=0,
@@ -421,7 +424,7 @@ def file_write_ceiling(outdir, nbytes, block=1 << 30):
             "what": "plain write() of one buffer in 1 GiB pieces, same directory"}
 
 
-def fits_wallclock(config3=True):
+def fits_wallclock(config3=True, kept=None):
     """FITS-cube wall-clock of make_aterm_image (the second half of the
     BASELINE.json metric; fit + evaluation + FITS write, host I/O included):
 
@@ -434,16 +437,24 @@ def fits_wallclock(config3=True):
       10 times (10.7 GB) per file, each file deleted when closed (the box has
       less disk than the cube); the unlink time is reported apart, and the
       box's plain file-write rate over one chunk's bytes is measured in the
-      same directory right after."""
+      same directory right after.
+
+    ``kept``: a dict that receives {config1 / config2: TemporaryDirectory}
+    holding the first run's cube, for the parity checks (the caller cleans
+    them up)."""
     import tempfile
     sys.path.insert(0, os.path.join(REPO, "tools"))
     import fits_wallclock as fw
     res = {}
     for name in ("config1", "config2"):
         best = None
-        for _ in range(2):
-            with tempfile.TemporaryDirectory() as d:
-                r = fw.run(name, d)
+        for k in range(2):
+            if k == 0 and kept is not None:
+                kept[name] = tempfile.TemporaryDirectory()
+                r = fw.run(name, kept[name].name)
+            else:
+                with tempfile.TemporaryDirectory() as d:
+                    r = fw.run(name, d)
             best = r if best is None or r["wall_s"] < best["wall_s"] else best
         res[name] = {"wall_s": best["wall_s"], "fits_bytes": best["fits_bytes"],
                      "screen_type": best["screen_type"],
@@ -590,6 +601,8 @@ class PowerSampler:
     def __init__(self, pci, path=None):
         import glob
         self.path, self.samples, self.source = path, [], path
+        self.pci = pci
+        self._smi_index = None  # amd-smi's index of this device (fallback)
         dev = f"/sys/bus/pci/devices/{pci}.0" if pci else None
         for name in ("power1_average", "power1_input"):
             if self.path:
@@ -615,10 +628,28 @@ class PowerSampler:
                 return int(fh.read().strip()) * 1e-6  # microwatts
         import subprocess
         exe = "/opt/rocm/bin/amd-smi" if os.path.exists("/opt/rocm/bin/amd-smi") else "amd-smi"
+        if self._smi_index is None:
+            # this rank's card among amd-smi's entries, by PCI address; no
+            # match: no reading (never another card's power)
+            lst = json.loads(subprocess.run([exe, "list", "--json"], capture_output=True,
+                                            text=True, timeout=10).stdout)
+            lst = lst if isinstance(lst, list) else [lst]
+            want = (self.pci or "").lower()
+            # self.pci is domain:bus:device ("0000:05:00"), amd-smi's bdf
+            # adds the function ("0000:05:00.0")
+            hit = [e.get("gpu") for e in lst
+                   if want and str(e.get("bdf", "")).lower().startswith(want + ".")]
+            if len(hit) != 1:
+                raise LookupError(f"amd-smi: no unique entry for PCI {self.pci}")
+            self._smi_index = hit[0]
         out = subprocess.run([exe, "metric", "-p", "--json"], capture_output=True,
                              text=True, timeout=10).stdout
         d = json.loads(out)
-        d = d[0] if isinstance(d, list) else d
+        d = d if isinstance(d, list) else [d]
+        d = [e for e in d if e.get("gpu") == self._smi_index]
+        if len(d) != 1:
+            raise LookupError(f"amd-smi metric: no entry for gpu {self._smi_index}")
+        d = d[0]
         p = d.get("power", d)
         v = p.get("socket_power", p.get("average_socket_power"))
         v = v.get("value") if isinstance(v, dict) else v
@@ -677,10 +708,17 @@ FP64_MFMA_PEAK_TFS = 78.6  # MI355X fp64 matrix peak (AMD spec, dense)
 I8_MFMA_PEAK_TOPS = 5000.0  # MI355X int8 matrix peak (dense; 2x bf16)
 
 
+STALE_COUNTERS = {}  # table -> the stale entry's library, for the line
+
+
 def _profile_entry(name, workload, kernel):
     """Entry of a profiles/<name>.json table (written by the tools/ that turn
     rocprofv3 PMC passes into per-launch figures) for this workload and
-    evaluation kernel, or None."""
+    evaluation kernel, or None -- also None when the entry was taken on
+    another build of the library than the one this process loaded (its
+    ``library_sha16``, tools/pmc_traffic.py): counters of an older kernel
+    are never reported as this one's (the line names the mismatch)."""
+    from ska_sdp_screen_fitting_amd._lib import library_identity
     path = os.path.join(REPO, "profiles", name)
     try:
         tab = json.load(open(path))
@@ -688,6 +726,9 @@ def _profile_entry(name, workload, kernel):
         return None
     for e in tab.get("entries", []):
         if e.get("workload") == workload and e.get("eval_kernel") == kernel:
+            if e.get("library_sha16") != library_identity()["sha16"]:
+                STALE_COUNTERS[f"{name}:{workload}:{kernel}"] = e.get("library_sha16")
+                return None
             return e
     return None
 
@@ -790,7 +831,8 @@ def child_leg(extra, what, timeout_s=420):
     idle meanwhile): its value, eval roofline, checks and wall time."""
     import subprocess
     cmd = [sys.executable, os.path.abspath(__file__), "--gpus", "1",
-           "--no-cpu-baseline", "--no-fits", "--no-side-legs", "--no-child-legs"] + extra
+           "--no-cpu-baseline", "--no-fits", "--no-side-legs", "--no-child-legs",
+           "--no-parity"] + extra
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     t0 = time.perf_counter()
     try:
@@ -876,7 +918,8 @@ def rehearse_cpu(args, dist, world, rank, sol, setup, A, A_total, a0):
                 "scaling": "strong", "vs_baseline": None, "dtype": "f64",
                 "data": "synthetic",
                 "config": {"workload": f"{args.workload}: {A_total} ant, rehearsal",
-                           "parallelism": f"ant-shard x{world}"},
+                           "parallelism": f"ant-shard x{world}",
+                           "schedule": args.schedule},
                 "rehearsal": ("cpu: self-launch + gloo setup collectives only, "
                               "no kernels"),
                 "setup_s": time.perf_counter() - t0, "dist": dist_info}
@@ -1029,6 +1072,31 @@ def tess_steps(args, ctx, torch, dev, dist, world, rank, coll_dev, sol, setup,
         dist.destroy_process_group()
 
 
+def pick_schedule(args, D, T):
+    """The step's schedule: time chunks, coefficient sets, CU reservation.
+    A function of the workload's shape and the command-line options only --
+    never of the world size -- so every N of the driver's scaling curve runs
+    the same schedule per GPU (the reference's fan-out, stationscreen.py:
+    1056-1077, gives each worker the same work; tests/test_bench_launch.py)."""
+    gain = args.screen == "gain"
+    # the amplitude outlier sigma couples every time of a (freq, station)
+    # block (Q6): the gain fit sees all times at once
+    n_chunks = 1 if gain else max(1, min(args.chunks, T))
+    n_sets = args.coef_sets if args.coef_sets > 0 else (
+        2 if gain and args.steps > 1 else 1)
+    pipelined = n_chunks > 1 or n_sets > 1
+    reserve_cus = args.reserve_cus
+    if reserve_cus < 0:
+        reserve_cus = 16 if D <= 32 and n_chunks > 1 else 0
+    on_reserved = args.fit_on_reserved
+    if on_reserved < 0:
+        on_reserved = 1 if D <= 32 else 0
+    return {"time_chunks": n_chunks, "coef_sets": n_sets, "pipelined": pipelined,
+            "reserve_cus": reserve_cus if pipelined else 0,
+            "fit_on_reserved": bool(on_reserved and pipelined and reserve_cus > 0),
+            "fit_priority": int(args.fit_priority) if pipelined else 0}
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -1096,7 +1164,7 @@ def main():
                                                  SF_OPT_EVAL_INT,
                                                  SF_OPT_EVAL_XCD_MAP)
     from ska_sdp_screen_fitting_amd.distributed import setup_shard
-    from ska_sdp_screen_fitting_amd._lib import SF_SCREEN_AMPLITUDE
+    from ska_sdp_screen_fitting_amd._lib import SF_SCREEN_AMPLITUDE, library_identity
     from ska_sdp_screen_fitting_amd.synthetic import (FIELD_DEC_DEG,
                                                       FIELD_RA_DEG,
                                                       FIELD_WIDTH_DEG,
@@ -1122,6 +1190,7 @@ def main():
     assert len(setup["x"]) == N
     log(f"shard ready: ant [{a0}, {a0 + A}) of {A_total}, {T * F * A} slots")
     if args.rehearse_cpu:
+        args.schedule = pick_schedule(args, D, T)
         return rehearse_cpu(args, dist, world, rank, sol, setup, A, A_total, a0)
 
     ctx = get_context(gpu)
@@ -1166,22 +1235,17 @@ def main():
             amp["resid"].append(torch.empty_like(v))
             amp["w_out"].append(torch.empty_like(w))
             amp["orders"].append(torch.empty((T, F, A), dtype=torch.int32, device=dev))
-        # the amplitude outlier sigma couples every time of a (freq,
-        # station) block (Q6): the fit sees all times at once
-        args.chunks = 1
 
     # time chunks (the solution layout is time-major, so a chunk is a
     # contiguous slice of every array); phase slots are independent, so the
-    # fit of one chunk can run while the previous chunk is evaluated
-    n_chunks = max(1, min(args.chunks, T))
+    # fit of one chunk can run while the previous chunk is evaluated;
     # coefficient sets: step k fits into and evaluates from set k % n_sets
-    sharded = world > 1 or (args.as_shard_of or 0) > 1
-    n_sets = args.coef_sets if args.coef_sets > 0 else (
-        2 if (args.screen == "gain" or sharded) and args.steps > 1 else 1)
+    sched = pick_schedule(args, D, T)
+    n_chunks, n_sets = sched["time_chunks"], sched["coef_sets"]
     coef_sets = [coef] + [torch.empty_like(coef) for _ in range(n_sets - 1)]
     amp_sets = ([amp["coef"]] + [[torch.empty_like(x) for x in amp["coef"]]
                                  for _ in range(n_sets - 1)]) if gain else None
-    pipelined = n_chunks > 1 or n_sets > 1
+    pipelined = sched["pipelined"]
     bounds = [(T * c // n_chunks, T * (c + 1) // n_chunks) for c in range(n_chunks)]
     # the eval saturates HBM without every CU: its stream leaves
     # --reserve-cus compute units (spread over the XCDs) to the fit stream, so
@@ -1194,9 +1258,7 @@ def main():
     # it runs on an unrestricted stream even when later fits are confined
     first_fit_stream = fit_stream
     if pipelined:
-        reserve_cus = args.reserve_cus
-        if reserve_cus < 0:
-            reserve_cus = 16 if D <= 32 and n_chunks > 1 else 0
+        reserve_cus = sched["reserve_cus"]
         if reserve_cus > 0:
             n_cu = ctx.device_cus()
             step = max(1, n_cu // reserve_cus)
@@ -1205,10 +1267,7 @@ def main():
             reserved = [min(n_cu - 1, k * step + k % 8) for k in range(reserve_cus)]
             masked_handle = ctx.stream_create(reserved)
             stream = torch.cuda.ExternalStream(masked_handle, device=dev)
-            on_reserved = args.fit_on_reserved
-            if on_reserved < 0:
-                on_reserved = 1 if D <= 32 else 0
-            if on_reserved:
+            if sched["fit_on_reserved"]:
                 keep = set(reserved)
                 fit_handle = ctx.stream_create([c for c in range(n_cu) if c not in keep])
                 fit_stream = torch.cuda.ExternalStream(fit_handle, device=dev)
@@ -1370,6 +1429,7 @@ def main():
         log("child legs: config 5, gain and tessellated on config 3")
         side.update(child_legs())
 
+    parity_failed = False
     if rank == 0:
         # SURVEY.md §8(d), per step; gain screens read three coefficient sets
         algo_bytes = S * (16 * P + 8 * D * (3 if gain else 1))
@@ -1418,7 +1478,7 @@ def main():
                 "parallelism": f"ant-shard x{world}",
                 "eval_sincos": "fp64" if args.precise_sincos else "fp32-after-fp64-reduction",
                 "eval_only": bool(args.eval_only),
-                "schedule": {"time_chunks": n_chunks, "coef_sets": n_sets},
+                "schedule": sched,
             },
             "roofline": {
                 "bound": "hbm",
@@ -1464,12 +1524,29 @@ def main():
                 "ms_per_step_in_pipeline": t_fit * 1e3,
                 "fp64_peak_tflops": FP64_MFMA_PEAK_TFS,
                 "kernels_pmc": {k: {"fp64_tflops": v.get("fp64_tflops"),
-                                    "avg_ms": v.get("avg_ms_under_pmc")}
+                                    "avg_ms": v.get("avg_ms"),
+                                    "avg_ms_under_pmc": v.get("avg_ms_under_pmc")}
                                 for k, v in (fe or {}).get("kernels", {}).items()},
+            "kernels_pmc_source": (fe or {}).get("source"),
             }
+        kept = {}
         if not args.no_fits and world == 1:
             log("FITS wall-clock legs")
-            line["fits_wallclock"] = fits_wallclock(config3=not args.no_fits_config3)
+            line["fits_wallclock"] = fits_wallclock(config3=not args.no_fits_config3,
+                                                    kept=kept)
+        if not args.no_parity:
+            # parity of the path against the reference's own outputs (golden
+            # files only), on the cubes the FITS legs wrote when they ran
+            log("parity checks")
+            sys.path.insert(0, os.path.join(REPO, "tools"))
+            import bench_parity
+            t_par = time.perf_counter()
+            line["parity"] = bench_parity.run(
+                gpu, flags, {k: v.name for k, v in kept.items()})
+            line["parity"]["wall_s"] = time.perf_counter() - t_par
+            parity_failed = not line["parity"]["all_ok"]
+        for v in kept.values():
+            v.cleanup()
         if not args.no_cpu_baseline and world == 1:
             log("CPU baseline")
             nw, rule = cpu_share()
@@ -1485,6 +1562,7 @@ def main():
                     v["gpu_fits_wall_s"] = fw[k]["wall_s"]
                     v["gpu_speedup"] = v["wall_s"] / fw[k]["wall_s"]
             line["cpu_baseline"]["legs"] = legs
+        line["library"] = dict(library_identity(), stale_counter_tables=dict(STALE_COUNTERS))
         print(json.dumps(line), flush=True)
     # release the CU-masked stream before the HIP runtime tears down
     torch.cuda.synchronize(dev)
@@ -1494,6 +1572,9 @@ def main():
             ctx.stream_destroy(h)
     if dist.is_initialized():
         dist.destroy_process_group()
+    if parity_failed:
+        log("PARITY FAILED: see the line's 'parity' object")
+        raise SystemExit(3)
 
 
 if __name__ == "__main__":

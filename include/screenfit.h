@@ -184,8 +184,17 @@ int sf_device_cus(sf_ctx* ctx, int* n_cu);
 #define SF_OPT_EVAL_INT 15
 /* SF_OPT_EVAL_WG_WAVES: waves per workgroup of the integer-digit register
  * tile -- 4 (0 = default: 256 pixels, 1 KiB store runs per (slot, plane)) or
- * 8 (512 pixels, 2 KiB runs).  Same bits. */
+ * 8 (512 pixels, 2 KiB runs).  Same bits.  It acts ONLY on the register tile
+ * (SF_EVAL_KERNEL_TILE / TILE3) running the integer-digit contraction
+ * (sf_get_eval_contraction == 1); the fp64 contraction, the LDS-staged
+ * kernels and SF_EVAL_KERNEL_SHB always run 4-wave workgroups and ignore it
+ * (the Python binding's eval_kernel() names the 8-wave variant when it runs). */
 #define SF_OPT_EVAL_WG_WAVES 16
+/* SF_OPT_FIT_EIG_WAVES: waves per flagged-direction mask of the subset-basis
+ * Jacobi in sf_kl_fit -- 1..4 (0 = default: 3).  Every count writes the same
+ * bits (the rotations and their per-element arithmetic do not depend on how
+ * a round's column pairs are split over the waves). */
+#define SF_OPT_FIT_EIG_WAVES 17
 #define SF_EVAL_KERNEL_AUTO 0
 #define SF_EVAL_KERNEL_TILE 1
 #define SF_EVAL_KERNEL_LDS4 2
@@ -246,6 +255,19 @@ int sf_kl_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,
  * flagged-direction masks whose subset basis was decomposed, and number of
  * slots that took the general (tiny-weight) path. */
 int sf_get_fit_stats(sf_ctx* ctx, int* n_masks, int* n_general);
+
+/* The subset bases the last sf_kl_fit decomposed (a test / inspection
+ * hook; every call renumbers and rebuilds its pool): up to max_masks
+ * entries, each its direction mask (masks_host[i], bit d = direction d
+ * unflagged, n bits set) and a [D][D] block whose leading n x n part holds
+ * the subset's eigenvectors (row = unflagged direction in index order,
+ * columns sorted by |lambda| descending) followed by D slots whose first n
+ * hold its eigenvalues (entries_host[i * (D*D + D)]); the rest of an entry
+ * is unspecified.  Entries are in the order the
+ * masks were numbered, which is not deterministic; *n_masks = how many
+ * exist.  Synchronises. */
+int sf_get_fit_pool(sf_ctx* ctx, uint64_t* masks_host, double* entries_host,
+                    int max_masks, int* n_masks);
 
 /*
  * Pixel grid of the a-term image: X[nx], Y[ny] screen coordinates of the

@@ -236,6 +236,11 @@ int sf_set_option(sf_ctx* ctx, int option, int value) {
                  "sf_set_option: eval workgroup waves must be 0, 4 or 8");
       ctx->eval_wg_waves = value;
       return SF_OK;
+    case SF_OPT_FIT_EIG_WAVES:
+      SF_REQUIRE(value >= 0 && value <= 4, SF_EINVAL,
+                 "sf_set_option: fit eig waves must be 0..4");
+      ctx->fit_eig_waves = value;
+      return SF_OK;
     default:
       set_error("sf_set_option: unknown option");
       return SF_EINVAL;
@@ -405,6 +410,29 @@ int sf_get_fit_stats(sf_ctx* ctx, int* n_masks, int* n_general) {
     SF_HIP(hipMemcpy(c, ctx->d_counters, sizeof(c), hipMemcpyDeviceToHost));
   if (n_masks) *n_masks = c[0];
   if (n_general) *n_general = c[2];
+  return SF_OK;
+}
+
+int sf_get_fit_pool(sf_ctx* ctx, uint64_t* masks_host, double* entries_host,
+                    int max_masks, int* n_masks) {
+  SF_REQUIRE(ctx && n_masks && max_masks >= 0, SF_EINVAL, "sf_get_fit_pool: bad argument");
+  SF_REQUIRE(max_masks == 0 || (masks_host && entries_host), SF_EINVAL,
+             "sf_get_fit_pool: NULL output");
+  SF_HIP(hipSetDevice(ctx->device));
+  SF_HIP(hipStreamSynchronize(ctx->stream));
+  int c0 = 0;
+  if (ctx->d_counters)
+    SF_HIP(hipMemcpy(&c0, ctx->d_counters, sizeof(int), hipMemcpyDeviceToHost));
+  const int n = ctx->pool_D == ctx->D && (size_t)c0 <= ctx->pool_cap ? c0 : 0;
+  *n_masks = n;
+  const int k = n < max_masks ? n : max_masks;
+  if (k > 0) {
+    const size_t entry = (size_t)ctx->D * ctx->D + ctx->D;
+    SF_HIP(hipMemcpy(masks_host, ctx->d_pool_mask, k * sizeof(uint64_t),
+                     hipMemcpyDeviceToHost));
+    SF_HIP(hipMemcpy(entries_host, ctx->d_pool, k * entry * sizeof(double),
+                     hipMemcpyDeviceToHost));
+  }
   return SF_OK;
 }
 

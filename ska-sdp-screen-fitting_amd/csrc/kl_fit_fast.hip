@@ -155,10 +155,12 @@ __global__ __launch_bounds__(256) void kl_assign_kernel(
 //    160 KiB (43,104 bytes, sized for D, let 3).
 __host__ __device__ inline int subset_ld(int D) { return ldo(D > 1 ? D - 1 : 1); }
 __host__ __device__ inline int subset_rows(int D) { return D > 1 ? D - 1 : 1; }
-#ifndef SF_EIG_WAVES
-#define SF_EIG_WAVES 3  // waves per mask of the subset Jacobi (wg_jacobi)
-#endif
-__global__ __launch_bounds__(64 * SF_EIG_WAVES) void kl_subset_eig_kernel(
+// NW: waves per mask of the subset Jacobi (wg_jacobi); the library runs 3
+// (kEigWavesDefault), SF_OPT_FIT_EIG_WAVES picks 1..4 -- the same bits at
+// every count (tests/test_gpu_parity.py::test_subset_jacobi_wave_count_*)
+constexpr int kEigWavesDefault = 3;
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void kl_subset_eig_kernel(
     const double* __restrict__ g_c, int D,
     const unsigned long long* __restrict__ pool_mask, int pool_cap,
     int* __restrict__ counters, double* __restrict__ pool) {
@@ -173,13 +175,13 @@ __global__ __launch_bounds__(64 * SF_EIG_WAVES) void kl_subset_eig_kernel(
   const int first = counters[1];
   const int last = min(counters[0], pool_cap);
   const int l = lane();
-  const bool w0 = threadIdx.x < 64;  // SF_EIG_WAVES waves per mask
+  const bool w0 = threadIdx.x < 64;  // NW waves per mask
   for (int id = first + blockIdx.x; id < last; id += gridDim.x) {
     const unsigned long long m = pool_mask[id];
     const bool in = (l < D) && ((m >> l) & 1ull);
     const int n = __popcll(m);
     if (n >= D) {  // cannot happen (full masks never enter the pool): flag it
-      if (threadIdx.x == 0) atomicOr(counters + 3, 2);
+      if (threadIdx.x == 0) atomicOr(counters + 3, 8);
       continue;
     }
     if (w0 && in) {
@@ -193,7 +195,7 @@ __global__ __launch_bounds__(64 * SF_EIG_WAVES) void kl_subset_eig_kernel(
       for (int q = 0; q < n; ++q) a[l * ld + q] = g_c[r * D + idx[q]];
     }
     __syncthreads();
-    wg_jacobi<SF_EIG_WAVES>(a, v, cs, pr, n, ld, 40);
+    wg_jacobi<NW>(a, v, cs, pr, n, ld, 40);
     __syncthreads();
     if (w0) wave_eig_order(a, n, ld, perm);
     double* e = pool + (size_t)id * (D * D + D);
@@ -889,14 +891,24 @@ static int number_and_decompose(sf_ctx* ctx, int* n_slow, int* n_nonuniform) {
     const size_t shm = (size_t)2 * subset_rows(D) * subset_ld(D) * sizeof(double) +
                        64 * sizeof(double2) + 96 * sizeof(int2) +
                        128 * sizeof(int);
-    if (shm > 64 * 1024)
-      SF_HIP(hipFuncSetAttribute(
-          reinterpret_cast<const void*>(&kl_subset_eig_kernel),
-          hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
     const int blocks = n_new < 8192 ? n_new : 8192;
-    hipLaunchKernelGGL(kl_subset_eig_kernel, dim3(blocks), dim3(64 * SF_EIG_WAVES), shm,
-                       ctx->stream, ctx->d_c, D, ctx->d_pool_mask,
-                       (int)ctx->pool_cap, ctx->d_counters, ctx->d_pool);
+    const int nw = ctx->fit_eig_waves > 0 ? ctx->fit_eig_waves : kEigWavesDefault;
+#define SF_LAUNCH_EIG(NW)                                                              \
+  do {                                                                                 \
+    if (shm > 64 * 1024)                                                               \
+      SF_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&kl_subset_eig_kernel<NW>), \
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm)); \
+    hipLaunchKernelGGL(kl_subset_eig_kernel<NW>, dim3(blocks), dim3(64 * NW), shm,     \
+                       ctx->stream, ctx->d_c, D, ctx->d_pool_mask, (int)ctx->pool_cap, \
+                       ctx->d_counters, ctx->d_pool);                                  \
+  } while (0)
+    switch (nw) {
+      case 1: SF_LAUNCH_EIG(1); break;
+      case 2: SF_LAUNCH_EIG(2); break;
+      case 4: SF_LAUNCH_EIG(4); break;
+      default: SF_LAUNCH_EIG(3); break;
+    }
+#undef SF_LAUNCH_EIG
     SF_HIP(hipGetLastError());
   }
   return SF_OK;
@@ -1086,13 +1098,16 @@ int launch_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,
                         hipMemcpyDeviceToHost, ctx->stream));
   SF_HIP(hipStreamSynchronize(ctx->stream));
   // error bits of the fit pass: 1 / 2 the mask table (lookup miss / subset
-  // basis missing), 4 the lean layout met a slot whose unflagged weights are
+  // basis missing), 8 a full mask in the subset pool, 4 the lean layout met a slot whose unflagged weights are
   // not uniform (kl_classify_kernel counted it uniform: an internal
   // inconsistency, the slot was left unwritten)
   SF_REQUIRE((err & 3) == 0, SF_EIO, "sf_kl_fit: internal mask table overflow");
   SF_REQUIRE((err & 4) == 0, SF_EIO,
              "sf_kl_fit: lean fit pass saw non-uniform weights in a slot "
              "classified uniform (slot left unwritten)");
+  SF_REQUIRE((err & 8) == 0, SF_EIO,
+             "sf_kl_fit: a mask with every direction unflagged entered the "
+             "subset-basis pool (its basis is the global one; left unbuilt)");
   return SF_OK;
 }
 

@@ -89,6 +89,7 @@ struct sf_ctx {
   size_t table_cap = 0;                  // power of two
   unsigned long long* d_pool_mask = nullptr;  // [pool_cap] mask of pool entry
   double* d_pool = nullptr;              // [pool_cap][D*D + D] (U_sub, lam)
+  int fit_eig_waves = 0;                 // SF_OPT_FIT_EIG_WAVES (0 = 3)
   size_t pool_cap = 0;
   int pool_D = 0;
   int* d_pos = nullptr;                  // [S] table slot of the current mask

@@ -172,6 +172,9 @@ __device__ inline int wave_jacobi(double* a, double* v, double2* cs, int2* pr,
       lds_sync();
       const double2 ri = own ? cs[i] : make_double2(1.0, 0.0);
       const int pir = own ? part[i] : 0;
+      // lanes that own no row read (and discard) row 0: every LDS address
+      // stays inside the n x ld matrices the caller sized
+      const int row = own ? i : 0;
       constexpr int CH = 4;  // column pairs per chunk
       for (int k0 = 0; k0 < npairs; k0 += CH) {
         double na[CH], nb[CH], nv[CH], nw[CH];
@@ -185,12 +188,12 @@ __device__ inline int wave_jacobi(double* a, double* v, double2* cs, int2* pr,
           qq[u] = pj;
           const double2 rj = cs[j];
           const double2 rq = cs[pj];
-          const double aij = a[i * ld + j];
-          const double aiq = a[i * ld + pj];
+          const double aij = a[row * ld + j];
+          const double aiq = a[row * ld + pj];
           const double apj = a[pir * ld + j];
           const double apq = a[pir * ld + pj];
-          const double vij = v[i * ld + j];
-          const double viq = v[i * ld + pj];
+          const double vij = v[row * ld + j];
+          const double viq = v[row * ld + pj];
           // row rotation then column rotation, summed symmetrically
           const double r_j = ri.x * aij + ri.y * apj;   // R_ij
           const double r_q = ri.x * aiq + ri.y * apq;   // R_i,pj
@@ -299,6 +302,9 @@ __device__ inline int wg_jacobi(double* a, double* v, double2* cs, int2* pr,
       __syncthreads();
       const double2 ri = own ? cs[i] : make_double2(1.0, 0.0);
       const int pir = own ? part[i] : 0;
+      // lanes that own no row read (and discard) row 0: every LDS address
+      // stays inside the n x ld matrices the caller sized
+      const int row = own ? i : 0;
       constexpr int CH = 4;  // column pairs per chunk
       for (int k0 = kb; k0 < ke; k0 += CH) {
         double na[CH], nb[CH], nv[CH], nw[CH];
@@ -312,12 +318,12 @@ __device__ inline int wg_jacobi(double* a, double* v, double2* cs, int2* pr,
           qq[u] = pj;
           const double2 rj = cs[j];
           const double2 rq = cs[pj];
-          const double aij = a[i * ld + j];
-          const double aiq = a[i * ld + pj];
+          const double aij = a[row * ld + j];
+          const double aiq = a[row * ld + pj];
           const double apj = a[pir * ld + j];
           const double apq = a[pir * ld + pj];
-          const double vij = v[i * ld + j];
-          const double viq = v[i * ld + pj];
+          const double vij = v[row * ld + j];
+          const double viq = v[row * ld + pj];
           const double r_j = ri.x * aij + ri.y * apj;
           const double r_q = ri.x * aiq + ri.y * apq;
           na[u] = rj.x * r_j + rj.y * r_q;

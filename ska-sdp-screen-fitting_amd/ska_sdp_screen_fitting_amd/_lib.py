@@ -37,6 +37,7 @@ SF_OPT_TESS_TILE = 13
 SF_OPT_TESS_BOX = 14
 SF_OPT_EVAL_INT = 15
 SF_OPT_EVAL_WG_WAVES = 16
+SF_OPT_FIT_EIG_WAVES = 17
 SF_EVAL_KERNEL_AUTO = 0
 SF_EVAL_KERNEL_TILE = 1
 SF_EVAL_KERNEL_LDS4 = 2
@@ -59,11 +60,29 @@ EVAL_KERNEL_NAMES = {SF_EVAL_KERNEL_TILE: "kl_eval_kernel",
 EXPORTED = (
     "sf_version", "sf_last_error", "sf_create", "sf_destroy", "sf_set_stream",
     "sf_synchronize", "sf_set_option", "sf_get_eval_kernel", "sf_get_eval_contraction", "sf_alloc", "sf_free", "sf_copy_h2d", "sf_copy_d2h",
-    "sf_set_basis", "sf_get_basis", "sf_kl_fit", "sf_get_fit_stats",
+    "sf_set_basis", "sf_get_basis", "sf_kl_fit", "sf_get_fit_stats", "sf_get_fit_pool",
     "sf_stream_create", "sf_stream_destroy", "sf_device_cus",
     "sf_set_grid", "sf_kl_eval", "sf_kl_eval_gain", "sf_kl_eval_sums",
     "sf_tess_fill", "sf_smooth",
 )
+
+
+_identity = {}
+
+
+def library_identity(path=None):
+    """sha256 (first 16 hex digits) and size of the library file this
+    process loads: the key the measurement tables under profiles/ carry, so
+    counters taken on another build are not reported as this one's."""
+    import hashlib
+    p = os.path.realpath(path or LIB_PATH)
+    if p not in _identity:
+        h = hashlib.sha256()
+        with open(p, "rb") as fh:
+            for blk in iter(lambda: fh.read(1 << 20), b""):
+                h.update(blk)
+        _identity[p] = {"sha16": h.hexdigest()[:16], "bytes": os.path.getsize(p)}
+    return dict(_identity[p])
 
 
 class ScreenFitError(RuntimeError):
@@ -116,6 +135,7 @@ def load_library(path=None):
             "sf_kl_fit": ([vp, vp, vp, c_int, c_int, c_int, ip,
                            ctypes.POINTER(FitParams), vp, vp, vp, vp], c_int),
             "sf_get_fit_stats": ([vp, ip, ip], c_int),
+            "sf_get_fit_pool": ([vp, vp, vp, c_int, ip], c_int),
             "sf_set_grid": ([vp, vp, c_int, vp, c_int], c_int),
             "sf_kl_eval": ([vp, vp, i64, vp, i64, ctypes.c_uint], c_int),
             "sf_stream_create": ([vp, ctypes.POINTER(c_int), c_int,
@@ -184,6 +204,7 @@ class Context:
         self.h = h
         self.D = 0
         self.grid = None
+        self.options = {}  # sf_set_option values set through this object
 
     def close(self):
         if self.h:
@@ -205,13 +226,21 @@ class Context:
     def set_option(self, option, value):
         _check(self.lib.sf_set_option(self.h, int(option), int(value)),
                "sf_set_option")
+        self.options[int(option)] = int(value)
 
     def eval_kernel(self, flags, gain=False):
-        """Name of the evaluation kernel sf_kl_eval runs for these flags."""
+        """Name of the evaluation kernel sf_kl_eval runs for these flags
+        (with the workgroup width when SF_OPT_EVAL_WG_WAVES = 8 takes effect:
+        the integer-digit contraction on the register tile only)."""
         k = ctypes.c_int()
         _check(self.lib.sf_get_eval_kernel(self.h, int(bool(gain)), int(flags),
                                            ctypes.byref(k)), "sf_get_eval_kernel")
-        return EVAL_KERNEL_NAMES[k.value]
+        name = EVAL_KERNEL_NAMES[k.value]
+        if (self.options.get(SF_OPT_EVAL_WG_WAVES, 0) == 8
+                and k.value in (SF_EVAL_KERNEL_TILE, SF_EVAL_KERNEL_TILE3)
+                and self.eval_contraction(flags, gain) == "i8-digits"):
+            name += " (8-wave workgroups)"
+        return name
 
     def eval_contraction(self, flags, gain=False):
         """'f64' (fp64 MFMAs) or 'i8-digits' (the integer-digit contraction)
@@ -269,6 +298,30 @@ class Context:
         _check(self.lib.sf_get_fit_stats(self.h, ctypes.byref(nm), ctypes.byref(ng)),
                "sf_get_fit_stats")
         return {"n_masks": nm.value, "n_general": ng.value}
+
+    def fit_pool(self):
+        """The subset bases decomposed so far (sf_get_fit_pool), sorted by
+        mask: (masks uint64 [n], entries float64 [n][D*D + D])."""
+        n = ctypes.c_int(0)
+        _check(self.lib.sf_get_fit_pool(self.h, None, None, 0, ctypes.byref(n)),
+               "sf_get_fit_pool")
+        D = self.D
+        masks = np.zeros(n.value, np.uint64)
+        ent = np.zeros((n.value, D * D + D))
+        if n.value:
+            _check(self.lib.sf_get_fit_pool(self.h, masks.ctypes.data, ent.ctypes.data,
+                                            n.value, ctypes.byref(n)), "sf_get_fit_pool")
+        order = np.argsort(masks, kind="stable")
+        masks, ent = masks[order], ent[order]
+        # only the leading n x n block and n eigenvalues of an n-direction
+        # mask are written; the rest of the entry is stale scratch
+        for k, m in enumerate(masks):
+            n = bin(int(m)).count("1")
+            u = ent[k, :D * D].reshape(D, D)
+            u[n:, :] = 0.0
+            u[:, n:] = 0.0
+            ent[k, D * D + n:] = 0.0
+        return masks, ent
 
     def set_grid(self, x, y):
         x = np.ascontiguousarray(x, dtype=np.float64)

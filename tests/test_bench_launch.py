@@ -123,3 +123,36 @@ def test_power_sampler_reads_hwmon_file(tmp_path):
     assert short.summary(1.0, 1.0) is None
     # nothing sampled (never entered): no power object in the line
     assert bench.PowerSampler(None).summary(1.0, 1.0) is None
+
+
+def test_schedule_is_the_same_at_every_world_size():
+    """The driver divides the N = 8 line's rate by the N = 1 line's: both
+    must run the same per-GPU schedule (time chunks, coefficient sets, CU
+    reservation).  bench.pick_schedule takes no world size; the rehearsal
+    line reports what every N would run."""
+    lines = {}
+    for n in (1, 8):
+        p = run_bench("--gpus", str(n), "--dist-backend", "gloo", "--workload", "tiny",
+                      "--rehearse-cpu", "--steps", "20")
+        assert p.returncode == 0, p.stderr[-2000:]
+        lines[n] = one_line(p)
+    s1, s8 = lines[1]["config"]["schedule"], lines[8]["config"]["schedule"]
+    assert s1 == s8
+    assert s1["coef_sets"] == 1 and s1["time_chunks"] == 1
+
+
+def test_pick_schedule_defaults():
+    """Phase screens: one chunk, one coefficient set (at any N); gain: two
+    sets over a multi-step run (fit of step k+1 beside the eval of step k)."""
+    import argparse
+    sys.path.insert(0, REPO)
+    import bench
+    base = dict(chunks=1, coef_sets=-1, reserve_cus=-1, fit_on_reserved=-1,
+                fit_priority=1, steps=20, screen="phase")
+    s = bench.pick_schedule(argparse.Namespace(**base), 20, 1000)
+    assert (s["time_chunks"], s["coef_sets"], s["pipelined"]) == (1, 1, False)
+    g = bench.pick_schedule(argparse.Namespace(**dict(base, screen="gain")), 20, 100)
+    assert (g["time_chunks"], g["coef_sets"], g["pipelined"]) == (1, 2, True)
+    assert g["reserve_cus"] == 0
+    c = bench.pick_schedule(argparse.Namespace(**dict(base, chunks=4)), 20, 100)
+    assert (c["time_chunks"], c["reserve_cus"], c["fit_on_reserved"]) == (4, 16, True)

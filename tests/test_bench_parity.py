@@ -1,0 +1,112 @@
+"""The parity checks every bench.py line carries (tools/bench_parity.py),
+checked on the CPU against the oracle: they pass on the reference's own
+outputs and catch a perturbed cube.  Plus the premises they rest on.
+"""
+
+import ast
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import FIELD, GOLDEN, REPO, load_golden
+from oracle import kl as okl
+from oracle import voronoi as ov
+
+sys.path.insert(0, os.path.join(REPO, "tools"))
+import bench_parity as bp  # noqa: E402
+
+
+def test_parity_module_never_touches_the_oracle():
+    """bench_parity is product-side measurement code: it may read golden
+    files, never import the oracle (the product path must not route
+    through it)."""
+    tree = ast.parse(open(os.path.join(REPO, "tools", "bench_parity.py")).read())
+    names = set()
+    for node in ast.walk(tree):
+        if isinstance(node, ast.Import):
+            names |= {a.name for a in node.names}
+        elif isinstance(node, ast.ImportFrom):
+            names.add(node.module or "")
+    assert not any(n.split(".")[0] == "oracle" for n in names), names
+
+
+@pytest.mark.parametrize("name", sorted(set(bp.FIT_SETS.values())))
+def test_fit_sets_have_no_ill_conditioned_slot(name):
+    """bench_parity compares every slot of its fit sets at 1e-8 with no
+    exclusion list: none of them has a slot where the reference's own fit is
+    chaotic (test_oracle_golden.ill_conditioned_slots)."""
+    from test_oracle_golden import ill_conditioned_slots
+    assert ill_conditioned_slots(load_golden(name)) == set()
+
+
+@pytest.mark.parametrize("name", sorted(set(bp.FIT_SETS.values())))
+def test_fit_sets_exercise_flags_and_orders(name):
+    """What the fit checks cover (reported in the line): synth20 / synth50
+    carry flagged entries (outliers zeroed, subset bases) and adapted
+    orders."""
+    g = load_golden(name)
+    if name != "fixture_kl":
+        assert (g["w_out"] == 0).sum() > 0
+        assert len(np.unique(g["orders"][g["orders"] > 0])) > 1
+    assert (g["orders"] == 0).any()  # the reference station
+
+
+def _config1_cube():
+    g = load_golden("fixture_kl")
+    ph = np.asarray(g["val"])
+    corr = ph - ph[:, :, 0:1, :]
+    from ska_sdp_screen_fitting_amd import voronoi_screen as vs
+    pos = vs.read_patch_positions(os.path.join(GOLDEN, "skymodel.txt"))
+    radec = np.array([pos[str(d).strip("[]")] for d in g["dir_names"]])
+    lab, _ = vs.tessellation_template(radec, FIELD["rad"], FIELD["dec"],
+                                      FIELD["width"], 0.2)
+    T, F, A, D = ph.shape
+    planes = ov.gather_planes(lab, corr.reshape(-1, D))
+    cube = ov.smooth(planes, bp.SMOOTH_PIX_CONFIG1)
+    return g, cube.reshape(T, F, A, 4, 17, 17)
+
+
+def test_config1_checks_on_oracle_cube():
+    """The oracle's config-1 cube (gather + Gaussian 0.5 px) passes the
+    patch criterion and the screens_.png colours; a patch pixel moved by
+    2e-4 fails the criterion, a colour step fails the PNG check."""
+    g, cube = _config1_cube()
+    err, n_in = bp.patch_criterion(cube, g, 17, 0.2)
+    assert n_in >= 5 and err < bp.PATCH_TOL["config1"]
+    (t, f, a, pol), ph = bp.png_select()
+    cpix = okl.cpix_matrix(g["piercepoints"], g["x17"], g["y17"])
+    kl = np.sin(okl.eval_phase_screens(g["coef"][t, f, a][None], cpix)[0])
+    kl = kl.astype(np.float32).reshape(17, 17)
+    assert bp.png_mismatch(cube[t, f, a, pol], kl, ph) == (0, 0)
+    px, py = bp._patch_pixels(g, 17, 0.2)
+    bad = cube.copy()
+    col, row = int(np.round(px[0])), int(np.round(py[0]))
+    bad[3, 2, 5, 1, row, col] += 2e-4
+    assert bp.patch_criterion(bad, g, 17, 0.2)[0] > bp.PATCH_TOL["config1"]
+    vor = cube[t, f, a, pol].copy()
+    # a median pixel moved by a few colour steps (vmin / vmax unchanged)
+    r, c = np.unravel_index(np.argsort(vor, axis=None)[vor.size // 2], vor.shape)
+    span = float(vor.max() - vor.min())
+    vor[r, c] += 0.05 * span  # ~13 colour steps
+    assert vor.max() > vor[r, c]
+    assert bp.png_mismatch(vor, kl, ph)[0] == 1
+
+
+def test_header_check_against_product_writer(tmp_path):
+    """The FITS writer's header for the fixture passes the card check; a
+    changed CDELT5 is named."""
+    import json
+    want = json.load(open(os.path.join(GOLDEN, "fixture_headers.json")))["17"]
+    hdr = {k: (True if k in ("SIMPLE", "EXTEND") else v) for k, v in want}
+    assert bp._header_check(hdr, 17) == []
+    hdr["CDELT5"] = hdr["CDELT5"] * (1 + 1e-12)
+    assert bp._header_check(hdr, 17) == ["CDELT5"]
+
+
+def test_entry_requires_every_equality():
+    e = bp._entry(1e-9, 1e-8, orders_equal=True, flags_equal=False)
+    assert not e["ok"]
+    assert bp._entry(1e-9, 1e-8, orders_equal=True, flags_equal=True)["ok"]
+    assert not bp._entry(float("nan"), 1e-8)["ok"]

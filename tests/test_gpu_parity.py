@@ -112,6 +112,46 @@ def test_fit_fast_equals_general_path(ctx, dev, name):
     np.testing.assert_allclose(fast[0][keep], gen[0][keep], rtol=0, atol=1e-9)
 
 
+def _wave_count_case(name):
+    if name != "config5-density":
+        return load_golden(name)
+    # config 5's flag density at D = 50: 1 % of (slot, dir) entries zero,
+    # 0.5 % outliers (flagged in pass 1) -- hundreds of distinct masks
+    from ska_sdp_screen_fitting_amd import geometry
+    from ska_sdp_screen_fitting_amd.synthetic import make_solutions
+    s = make_solutions(n_ant=12, n_time=40, n_freq=2, n_dir=50, seed=55,
+                       flag_frac=0.01, outlier_frac=0.005)
+    pp, _, _ = geometry.piercepoints(s.dir_radec)
+    return dict(val=s.val, weight=s.weight, ant_pos=s.ant_pos, piercepoints=pp,
+                ref_ant=okl.reference_station(s.weight), order=20)
+
+
+@pytest.mark.parametrize("name", ["synth50", "config5-density", "synth20"])
+def test_subset_jacobi_wave_count_is_bit_identical(ctx, dev, name):
+    """The subset-basis Jacobi (kl_subset_eig_kernel -> wg_jacobi<NW>,
+    stationscreen.py:390-430 / :495-499 per flagged mask) on 1, 2, 3 (the
+    default) and 4 waves per mask: the same pool of subset bases, bit for
+    bit, and the same orders, flags, coefficients and residuals."""
+    from ska_sdp_screen_fitting_amd._lib import SF_OPT_FIT_EIG_WAVES
+    g = _wave_count_case(name)
+    runs = {}
+    try:
+        for nw in (3, 1, 2, 4):
+            ctx.set_option(SF_OPT_FIT_EIG_WAVES, nw)
+            out = gpu_fit(ctx, dev, g)
+            runs[nw] = (out, ctx.fit_pool())
+    finally:
+        ctx.set_option(SF_OPT_FIT_EIG_WAVES, 0)
+    (ref_out, (ref_masks, ref_pool)) = runs[3]
+    assert len(ref_masks) > (100 if name == "config5-density" else 0)
+    assert len(np.unique(ref_masks)) == len(ref_masks)
+    for nw, (out, (masks, pool)) in runs.items():
+        assert np.array_equal(masks, ref_masks), nw
+        assert np.array_equal(pool.view(np.uint64), ref_pool.view(np.uint64)), nw
+        for a, b in zip(out, ref_out):
+            assert np.array_equal(a.view(np.uint8), b.view(np.uint8)), nw
+
+
 @pytest.mark.parametrize("name", ["synth20", "synth12tiny", "fixture_kl"])
 def test_fit_two_slots_per_wave_is_bit_identical(ctx, dev, name):
     """Two slots per wavefront (D <= 32) must not change a single bit: the

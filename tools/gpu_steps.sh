@@ -24,6 +24,10 @@ out=$1
 shift
 mkdir -p "$out"
 export TMPDIR=/tmp
+# the library every step of this session loads (ab: steps name their own)
+python3 -c "import sys, json; sys.path.insert(0, 'ska-sdp-screen-fitting_amd'); \
+from ska_sdp_screen_fitting_amd._lib import library_identity; \
+print(json.dumps(library_identity()))" > "$out/library.json" 
 T_TEST=${T_TEST:-400}
 T_BENCH=${T_BENCH:-300}
 for step in "$@"; do

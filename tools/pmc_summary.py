@@ -13,7 +13,12 @@ fractions:
 * wait / issue / active shares of SQ_WAVE_CYCLES
 * fp64 FLOP       = 64 x (2 FMA + MUL + ADD + TRANS) + 2048 x MFMA_F64 ops
 
-    python tools/pmc_summary.py DIR --kernel kl_eval [--cus 256] [--json]
+    python tools/pmc_summary.py DIR --kernel kl_eval [--cus 256] [--trace TDIR]
+
+``--trace TDIR``: a --kernel-trace run of the same command (pmc_passes.sh
+set ``trace``); ``avg_ms_trace`` is then the kernel's mean duration per call
+over the same full-grid dispatches without counter collection (PMC passes
+serialise and slow the dispatches), and the derived rates use it.
 """
 import argparse
 import csv
@@ -39,6 +44,19 @@ def load(d, kernel):
     return per, meta
 
 
+def trace_ms(d, kernel, big):
+    """Mean duration (ms) per call of ``kernel``'s dispatches with grid
+    ``big`` (the PMC grouping's full grid) in the kernel traces under d."""
+    durs = []
+    for path in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+        rows = [r for r in csv.DictReader(open(path)) if kernel in r["Kernel_Name"]]
+        for r in rows:
+            g = int(r.get("Grid_Size") or r.get("Grid_Size_X"))
+            if g == big:
+                durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6)
+    return (sum(durs) / len(durs), len(durs)) if durs else (None, 0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
@@ -46,6 +64,7 @@ def main():
                     help="substring of the full kernel name (template args included)")
     ap.add_argument("--cus", type=int, default=256)
     ap.add_argument("--json", action="store_true")
+    ap.add_argument("--trace", default=None)
     ap.add_argument("--group", type=int, default=0,
                     help="dispatches per call (default: a call ends at a "
                     "partial-grid dispatch)")
@@ -90,6 +109,20 @@ def main():
            "work_items_per_call": sum(meta[k][0] for k in groups[0]),
            "avg_ms_under_pmc": dur, "vgpr": meta[k0][3],
            "lds_bytes": meta[k0][4], "counters": avg}
+    # rates over the traced duration when a trace is given (the counters
+    # are counts, independent of the slow-down under collection)
+    if a.trace:
+        tms, tn = trace_ms(a.trace, a.kernel, big)
+        calls = max(1, round(sum(len(g) for g in groups) / len(groups)))
+        if tms is not None:
+            res["avg_ms_trace"] = tms * calls
+            res["trace_dispatches"] = tn
+            rate_ms = tms * calls
+        else:
+            res["avg_ms_trace"] = None
+            rate_ms = dur
+    else:
+        rate_ms = dur
     g = avg.get("GRBM_GUI_ACTIVE")
     simd_cyc = g / 8 * a.cus * 4 if g else None
     d = {}
@@ -112,11 +145,11 @@ def main():
     if all(c in avg for c in f64):
         vflop = 64 * (2 * avg[f64[0]] + avg[f64[1]] + avg[f64[2]] + avg[f64[3]])
         d["valu_fp64_flop"] = vflop
-        d["valu_fp64_tflops"] = vflop / (dur * 1e-3) / 1e12
+        d["valu_fp64_tflops"] = vflop / (rate_ms * 1e-3) / 1e12
     if "SQ_INSTS_VALU_MFMA_MOPS_F64" in avg:
         # MOPS counts 512-flop units per the rocprof-compute convention
         d["mfma_f64_flop"] = 512 * avg["SQ_INSTS_VALU_MFMA_MOPS_F64"]
-        d["mfma_f64_tflops"] = d["mfma_f64_flop"] / (dur * 1e-3) / 1e12
+        d["mfma_f64_tflops"] = d["mfma_f64_flop"] / (rate_ms * 1e-3) / 1e12
     if "SQ_INSTS_VALU_MFMA_F64" in avg:
         # v_mfma_f64_16x16x4_f64: 16 x 16 x 4 x 2 flop per wave-instruction
         d["mfma_f64_flop_from_insts"] = 2048 * avg["SQ_INSTS_VALU_MFMA_F64"]

@@ -23,11 +23,24 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def summary(d, kernel):
-    out = subprocess.run([sys.executable, os.path.join(REPO, "tools", "pmc_summary.py"),
-                          d, "--kernel", kernel], check=True, capture_output=True,
-                         text=True).stdout
+def summary(d, kernel, trace=None):
+    cmd = [sys.executable, os.path.join(REPO, "tools", "pmc_summary.py"), d,
+           "--kernel", kernel]
+    if trace:
+        cmd += ["--trace", trace]
+    out = subprocess.run(cmd, check=True, capture_output=True, text=True).stdout
     return json.loads(out)
+
+
+def library_of(d):
+    """The library identity pmc_passes.sh recorded beside the passes (in the
+    pass directory or its parent); no identity, no table entry."""
+    for c in (d, os.path.dirname(os.path.normpath(d))):
+        f = os.path.join(c, "library.json")
+        if os.path.exists(f):
+            return json.load(open(f))
+    raise SystemExit(f"no library.json in {d} or its parent: counters without "
+                     "the identity of the library they were taken on are not kept")
 
 
 def upsert(path, entry):
@@ -61,6 +74,8 @@ def main():
     ap.add_argument("--fit-dir", help="pmc_passes.sh dir with valu/ occ/ of a "
                     "fit + eval run: fp64 FLOP/s of the fit kernels")
     ap.add_argument("--label", default="")
+    ap.add_argument("--fit-trace-dir", help="a --kernel-trace run of the fit command "
+                    "(pmc_passes.sh set trace): the fit kernels' durations")
     a = ap.parse_args()
     algo = a.slots * (16 * a.grid * a.grid + 8 * a.n_dir * a.coef_sets)
     if a.traffic_dir:
@@ -69,6 +84,7 @@ def main():
         wb, fb = d["write_bytes"], d["fetch_bytes_x2"]
         entry = {
             "workload": a.workload, "kernel": r["kernel"], "eval_kernel": a.eval_kernel,
+            "library_sha16": library_of(a.traffic_dir)["sha16"],
             "flags": a.flags, "chunks": a.chunks, "launches_averaged": r["dispatches"],
             "write_bytes": wb, "fetch_bytes_corrected_x2": fb,
             "hbm_bytes_per_launch": wb + fb,
@@ -81,7 +97,7 @@ def main():
         upsert(os.path.join(REPO, "profiles", "traffic.json"), entry)
         print(json.dumps(entry, indent=1))
     if a.fit_dir:
-        entry = fit_entry(a.fit_dir, a.workload, a.label)
+        entry = fit_entry(a.fit_dir, a.workload, a.label, a.fit_trace_dir)
         upsert(os.path.join(REPO, "profiles", "fit_flops.json"), entry)
         print(json.dumps(entry, indent=1))
     if a.mfma_dir:
@@ -89,6 +105,7 @@ def main():
         d = r["derived"]
         entry = {
             "workload": a.workload, "kernel": r["kernel"], "eval_kernel": a.eval_kernel,
+            "library_sha16": library_of(a.mfma_dir)["sha16"],
             "mfma_busy_frac": d.get("mfma_busy_frac"),
             "valu_busy_frac": d.get("valu_busy_frac"),
             "cyc_per_mfma_f64": d.get("cyc_per_mfma_f64"),
@@ -105,27 +122,34 @@ def main():
         print(json.dumps(entry, indent=1))
 
 
-def fit_entry(d, workload, label):
+def fit_entry(d, workload, label, trace=None):
     """fp64 FLOP/s of the fit kernels (VALU: 64 x (2 FMA + MUL + ADD + TRANS)
-    per wave-instruction, SQ_INSTS_VALU_*_F64; no MFMA in the fit)."""
+    per wave-instruction, SQ_INSTS_VALU_*_F64; no MFMA in the fit): flop
+    counts from the PMC passes, durations from the kernel trace of the same
+    command when given (``avg_ms``), else the slower durations under
+    collection (``avg_ms_under_pmc``)."""
     kernels = {}
     for k in ("kl_fit_pass_kernel", "kl_subset_eig_kernel", "kl_classify_kernel",
               "kl_assign_kernel", "kl_fit_general_kernel"):
         try:
-            r = summary(d, k)
+            r = summary(d, k, trace)
         except subprocess.CalledProcessError:
             continue
         dd = r["derived"]
         kernels[k] = {"kernel": r["kernel"], "dispatches_averaged": r["dispatches"],
+                      "avg_ms": r.get("avg_ms_trace"),
                       "avg_ms_under_pmc": r["avg_ms_under_pmc"],
                       "fp64_flop_per_launch": dd.get("valu_fp64_flop"),
                       "fp64_tflops": dd.get("valu_fp64_tflops"),
                       "valu_busy_frac": dd.get("valu_busy_frac")}
     return {"workload": workload, "eval_kernel": "fit", "kernels": kernels,
+            "library_sha16": library_of(d)["sha16"],
             "source": os.path.relpath(d, REPO), "label": label,
+            "trace": os.path.relpath(trace, REPO) if trace else None,
             "note": "largest-grid launch of each fit kernel in a bench.py "
                     "--steps 1 --warmup 0 run under rocprofv3 --pmc (valu, occ "
-                    "passes); fp64 VALU peak 78.6 TFLOP/s"}
+                    "passes), durations and rates from a --kernel-trace run of "
+                    "the same command; fp64 VALU peak 78.6 TFLOP/s"}
 
 
 if __name__ == "__main__":
