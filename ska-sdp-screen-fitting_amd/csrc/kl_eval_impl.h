@@ -16,6 +16,20 @@ namespace sf {
 
 typedef double v4d __attribute__((ext_vector_type(4)));
 
+// Energy attribution builds (tools/energy_variants.sh; never the shipped
+// library): the register tile with one component removed, so the board
+// power of each variant splits a kernel's joules per output byte into its
+// parts -- 1: contraction only (no sincos / amplitude: the reduced phase and
+// the raw log-amplitudes are stored), 2: epilogue only (no MFMA: the
+// accumulators take a loaded coefficient / digit row), 3: stores only
+// (neither: lane-dependent constants), 4: no evaluation kernel work at all
+// (the launch returns at once; the integer path's slot-digit prepass still
+// runs).  The same stores in the same pattern in every variant.
+#ifndef SF_EVAL_ENERGY_DIAG
+#define SF_EVAL_ENERGY_DIAG 0
+#endif
+constexpr int kEnergyDiag = SF_EVAL_ENERGY_DIAG;
+
 
 
 // f64 16x16x4 accumulator layout on gfx950: lane l, register r holds
@@ -376,6 +390,8 @@ __global__ __launch_bounds__(64 * NWV, MINW) void kl_eval_kernel(
     unsigned* __restrict__ sums, float* __restrict__ trash, double rev_thr,
     DigArgs dg) {
   constexpr int kFrag = KS * kTiles * 64;  // Cpix doubles of a wave pixel block
+  if constexpr (kEnergyDiag == 4) return;
+  constexpr bool kNoContract = kEnergyDiag == 2 || kEnergyDiag == 3;
   // IC: the integer-digit contraction (kl_eval_int.h) instead of the fp64
   // MFMAs; slots it cannot carry take the fp64 contraction with the Cpix
   // fragments read from memory.  IC + SHB: the pixel digit fragments of the
@@ -547,6 +563,18 @@ __global__ __launch_bounds__(64 * NWV, MINW) void kl_eval_kernel(
       if constexpr (!IC) {
 #pragma unroll
         for (int t = 0; t < kTiles; ++t) acc[t] = v4d{a0, a0, a0, a0};
+        if constexpr (kNoContract) {
+          // energy diagnostic: a loaded coefficient instead of the products
+#pragma unroll
+          for (int t = 0; t < kTiles; ++t) acc[t] += af[t % KS];
+          if constexpr (GAIN) {
+#pragma unroll
+            for (int t = 0; t < kTiles; ++t) {
+              accx[t] = v4d{ax[t % KS], ax[t % KS], ax[t % KS], ax[t % KS]};
+              accy[t] = v4d{ay[t % KS], ay[t % KS], ay[t % KS], ay[t % KS]};
+            }
+          }
+        } else {
 #pragma unroll
         for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
@@ -566,6 +594,7 @@ __global__ __launch_bounds__(64 * NWV, MINW) void kl_eval_kernel(
               accx[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ax[kk], bval(kk, t), accx[t], 0, 0, 0);
               accy[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ay[kk], bval(kk, t), accy[t], 0, 0, 0);
             }
+        }
         }
         // fixed point or exact by ONE wave-uniform branch per group (per-row
         // branches measured 4 % slower at D = 50); gain screens scrub the
@@ -595,7 +624,10 @@ __global__ __launch_bounds__(64 * NWV, MINW) void kl_eval_kernel(
 #pragma unroll
         for (int t = 0; t < kTiles; ++t) {
           v4i R;
-          if constexpr (SHB) {
+          if constexpr (kNoContract) {
+            R = wp.w[t % kDigits];  // energy diagnostic: no MFMA
+            if constexpr (!SHB) R ^= bd[t][0];
+          } else if constexpr (SHB) {
             const v4i* bs = reinterpret_cast<const v4i*>(bsh);
             v4i bt[kDigits];
 #pragma unroll
@@ -680,6 +712,21 @@ __global__ __launch_bounds__(64 * NWV, MINW) void kl_eval_kernel(
 #pragma unroll
         for (int t = 0; t < kTiles; ++t) {
           float sf, cf;
+          if constexpr (kEnergyDiag == 3) {
+            // energy diagnostic: stores only
+            pv[0][t] = pv[2][t] = (float)(l + t);
+            pv[1][t] = pv[3][t] = (float)(r - t);
+            continue;
+          } else if constexpr (kEnergyDiag == 1) {
+            // energy diagnostic: the contraction's values, no sincos / exp2
+            pv[0][t] = pv[2][t] = fr[t];
+            pv[1][t] = pv[3][t] = fr[t];
+            if constexpr (GAIN) {
+              pv[2][t] = (float)accx[t][r];
+              pv[3][t] = (float)accy[t][r];
+            }
+            continue;
+          }
           if (GAIN) {
             // a NaN phase stays NaN through A * cos and is scrubbed below,
             // as the reference scrubs the product (screen.py:368-378)

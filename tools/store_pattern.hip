@@ -1,0 +1,197 @@
+// Store-pattern probe (round 5): which ORDER of the evaluation's output
+// stores does HBM take fastest, with no loads and no compute at all?
+//
+// Round 5's energy variants (SF_EVAL_ENERGY_DIAG, profiles/round5_energy.json)
+// showed the register-tile evaluations (config 5, gain) run as fast with the
+// contraction and the epilogue removed as with them, at clocks from 2.0 to
+// 2.4 GHz: their rate is set by the store stream, not by joules.  This probe
+// writes a ring of S slots x 4 planes x P float32 (the eval's [slot][4][y][x]
+// layout) in the eval kernels' work-item orders and a few others:
+//
+//   rows4  the register tile: a wave owns 64 pixels, a store instruction
+//          covers 4 slot rows x 256 B (lane l -> slot row (l >> 4) + 4 r),
+//          NW waves per workgroup, G 16-slot groups per work item
+//   contig the LDS-staged kernels: a workgroup owns RUN pixels, a store
+//          instruction covers 1 KiB of one (slot, plane) row
+//   lin    one float4 per thread in address order (torch fill_)
+//
+// Work items map to the XCDs as eval_block (kl_eval_impl.h): contiguous
+// pixel blocks per XCD (x0) or interleaved (x1), optionally B pixel bands.
+//   hipcc --offload-arch=gfx950 -O3 tools/store_pattern.hip -o tools/store_pattern
+//   tools/store_pattern [GiB]
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void st(float* p, v4f v) {
+  __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(p));
+}
+
+// eval_block of kl_eval_impl.h (bands: lb = log2 B)
+__device__ __forceinline__ void item(long bb, long n_pb, long n_sc, int lb, int xi,
+                                     long& pb, long& sc) {
+  long band = 0;
+  if (lb) {
+    n_pb >>= lb;
+    const long per_band = n_pb * n_sc;
+    band = bb / per_band;
+    bb -= band * per_band;
+  }
+  if ((n_pb & 7) == 0) {
+    const long per = n_pb >> 3;
+    const long x = bb & 7, i = bb >> 3;
+    pb = xi ? (i % per) * 8 + x : x * per + (i % per);
+    sc = i / per;
+  } else {
+    pb = bb % n_pb;
+    sc = bb / n_pb;
+  }
+  pb += band * n_pb;
+}
+
+__global__ __launch_bounds__(256) void lin(float* out, long n4) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i < n4) st(out + 4 * i, v4f{1.f, 2.f, 3.f, (float)threadIdx.x});
+}
+
+// register tile: NW waves x 64 pixels per workgroup, G groups of 16 slots
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void rows4(float* out, long P, long S, long n_pb,
+                                                 long n_sc, int G, int lb, int xi) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  long pb, sc;
+  item(blockIdx.x, n_pb, n_sc, lb, xi, pb, sc);
+  if (sc >= n_sc) return;
+  const long p0 = (pb * NW + w) * 64 + (l & 15) * 4;
+  if (p0 >= P) return;
+  const v4f v = {1.f, 2.f, 3.f, (float)l};
+  for (int g = 0; g < G; ++g) {
+    const long s0 = (sc * G + g) * 16;
+    if (s0 >= S) return;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long s = s0 + (l >> 4) + 4 * r;
+      if (s < S) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) st(out + (s * 4 + q) * P + p0, v);
+      }
+    }
+  }
+}
+
+// LDS-staged pattern: a workgroup of NW waves owns RUN pixels; wave w writes
+// slots w * (16 / NW) + j of each group, 1 KiB per store instruction
+template <int NW, int RUN>
+__global__ __launch_bounds__(64 * NW) void contig(float* out, long P, long S, long n_pb,
+                                                  long n_sc, int G, int lb, int xi) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  long pb, sc;
+  item(blockIdx.x, n_pb, n_sc, lb, xi, pb, sc);
+  if (sc >= n_sc) return;
+  const long pix0 = pb * RUN;
+  const v4f v = {1.f, 2.f, 3.f, (float)l};
+  for (int g = 0; g < G; ++g) {
+    const long s0 = (sc * G + g) * 16;
+    if (s0 >= S) return;
+    for (int j = 0; j < 16 / NW; ++j) {
+      const long s = s0 + w * (16 / NW) + j;
+      if (s >= S) continue;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int c = 0; c < RUN / 256; ++c) {
+          const long p = pix0 + c * 256 + 4 * l;
+          if (p < P) st(out + (s * 4 + q) * P + p, v);
+        }
+    }
+  }
+}
+
+int main(int argc, char** argv) {
+  const long gib = argc > 1 ? atol(argv[1]) : 16;
+  const long bytes = gib << 30;
+  float* out;
+  if (hipMalloc(&out, bytes) != hipSuccess) return 1;
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  auto time = [&](const char* name, long wrote, auto launch) {
+    launch();
+    (void)hipDeviceSynchronize();
+    float tot = 0.f, best = 1e30f;
+    const int reps = 8;
+    for (int r = 0; r < reps; ++r) {
+      (void)hipEventRecord(e0);
+      launch();
+      (void)hipEventRecord(e1);
+      (void)hipEventSynchronize(e1);
+      float ms;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      tot += ms;
+      if (ms < best) best = ms;
+    }
+    const double gbs = wrote / (tot / reps * 1e-3) / 1e9;
+    printf("%-44s %7.1f GB/s  frac %.3f  (mean %.3f ms, best %.3f)\n", name, gbs,
+           gbs / 8000.0, tot / reps, best);
+    fflush(stdout);
+  };
+  const long n4 = bytes / 16;
+  time("lin (fill_ order)", bytes, [&] {
+    hipLaunchKernelGGL(lin, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, 0, out, n4);
+  });
+  char name[128];
+  for (long N : {256L, 512L}) {
+    const long P = N * N;
+    const long S = bytes / (16 * P);
+    const long wrote = S * 16 * P;
+    // the register tile (4 waves; the integer tile also 8) by groups / map / bands
+    for (int nw : {4, 8}) {
+      const long n_pb = P / (64 * nw);
+      for (int G : {1, 4, 16, 64}) {
+        const long n_sc = (S + 16 * G - 1) / (16 * G);
+        for (int xi : {0, 1})
+          for (int lb : {0, 3}) {
+            if (lb && (n_pb % (8 << lb))) continue;
+            if (N == 256 && lb) continue;
+            snprintf(name, sizeof name, "rows4  %ld^2 nw%d g%-2d x%d b%d", N, nw, G, xi, 1 << lb);
+            time(name, wrote, [&] {
+              if (nw == 4)
+                hipLaunchKernelGGL(rows4<4>, dim3((unsigned)(n_pb * n_sc)), dim3(256), 0, 0,
+                                   out, P, S, n_pb, n_sc, G, lb, xi);
+              else
+                hipLaunchKernelGGL(rows4<8>, dim3((unsigned)(n_pb * n_sc)), dim3(512), 0, 0,
+                                   out, P, S, n_pb, n_sc, G, lb, xi);
+            });
+          }
+      }
+    }
+    // the LDS-staged shapes: 4 waves / 1 KiB, 8 / 2 KiB, 16 / 4 KiB runs
+    for (int shape = 0; shape < 3; ++shape) {
+      const int run = 256 << shape;
+      const long n_pb = P / run;
+      for (int G : {1, 4, 16, 64}) {
+        const long n_sc = (S + 16 * G - 1) / (16 * G);
+        for (int xi : {0, 1}) {
+          snprintf(name, sizeof name, "contig %ld^2 run%-4d g%-2d x%d", N, run * 4, G, xi);
+          time(name, wrote, [&] {
+            const unsigned nb = (unsigned)(n_pb * n_sc);
+            if (shape == 0)
+              hipLaunchKernelGGL((contig<4, 256>), dim3(nb), dim3(256), 0, 0, out, P, S, n_pb,
+                                 n_sc, G, 0, xi);
+            else if (shape == 1)
+              hipLaunchKernelGGL((contig<8, 512>), dim3(nb), dim3(512), 0, 0, out, P, S, n_pb,
+                                 n_sc, G, 0, xi);
+            else
+              hipLaunchKernelGGL((contig<16, 1024>), dim3(nb), dim3(1024), 0, 0, out, P, S,
+                                 n_pb, n_sc, G, 0, xi);
+          });
+        }
+      }
+    }
+  }
+  (void)hipFree(out);
+  return 0;
+}
