@@ -18,7 +18,8 @@
 // Work items map to the XCDs as eval_block (kl_eval_impl.h): contiguous
 // pixel blocks per XCD (x0) or interleaved (x1), optionally B pixel bands.
 //   hipcc --offload-arch=gfx950 -O3 tools/store_pattern.hip -o tools/store_pattern
-//   tools/store_pattern [GiB]
+//   tools/store_pattern [GiB [1]]   (1: the rhythm sweep -- s_sleep "compute"
+//   between store bursts, a barrier per group, LDS-capped occupancy)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -110,6 +111,66 @@ __global__ __launch_bounds__(64 * NW) void contig(float* out, long P, long S, lo
   }
 }
 
+// the same two patterns with the eval's rhythm: `sl` s_sleep(1) ticks
+// (~64 clocks each) of "compute" before each group's stores, a workgroup
+// barrier per group (bar), and dynamic LDS to cap workgroups per CU
+template <int NW, int RUN>
+__global__ __launch_bounds__(64 * NW) void contig_t(float* out, long P, long S, long n_pb,
+                                                    long n_sc, int G, int xi, int sl, int bar) {
+  extern __shared__ float pad[];
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (sl < 0) pad[threadIdx.x] = 0.f;  // never: keeps the LDS allocation
+  long pb, sc;
+  item(blockIdx.x, n_pb, n_sc, 0, xi, pb, sc);
+  if (sc >= n_sc) return;
+  const long pix0 = pb * RUN;
+  const v4f v = {1.f, 2.f, 3.f, (float)l};
+  for (int g = 0; g < G; ++g) {
+    const long s0 = (sc * G + g) * 16;
+    if (s0 >= S) return;  // uniform per workgroup
+    for (int z = 0; z < sl; ++z) __builtin_amdgcn_s_sleep(1);
+    if (bar) __syncthreads();
+    for (int j = 0; j < 16 / NW; ++j) {
+      const long s = s0 + w * (16 / NW) + j;
+      if (s >= S) continue;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int c = 0; c < RUN / 256; ++c) {
+          const long p = pix0 + c * 256 + 4 * l;
+          if (p < P) st(out + (s * 4 + q) * P + p, v);
+        }
+    }
+  }
+}
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void rows4_t(float* out, long P, long S, long n_pb,
+                                                   long n_sc, int G, int lb, int xi, int sl) {
+  extern __shared__ float pad[];
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (sl < 0) pad[threadIdx.x] = 0.f;
+  long pb, sc;
+  item(blockIdx.x, n_pb, n_sc, lb, xi, pb, sc);
+  if (sc >= n_sc) return;
+  const long p0 = (pb * NW + w) * 64 + (l & 15) * 4;
+  if (p0 >= P) return;
+  const v4f v = {1.f, 2.f, 3.f, (float)l};
+  for (int g = 0; g < G; ++g) {
+    const long s0 = (sc * G + g) * 16;
+    if (s0 >= S) return;
+    for (int z = 0; z < sl; ++z) __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long s = s0 + (l >> 4) + 4 * r;
+      if (s < S) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) st(out + (s * 4 + q) * P + p0, v);
+      }
+    }
+  }
+}
+
 int main(int argc, char** argv) {
   const long gib = argc > 1 ? atol(argv[1]) : 16;
   const long bytes = gib << 30;
@@ -118,9 +179,14 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&contig_t<16, 1024>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 131584);
   auto time = [&](const char* name, long wrote, auto launch) {
     launch();
-    (void)hipDeviceSynchronize();
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+      printf("%-44s launch failed\n", name);
+      return;
+    }
     float tot = 0.f, best = 1e30f;
     const int reps = 8;
     for (int r = 0; r < reps; ++r) {
@@ -143,6 +209,40 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL(lin, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, 0, out, n4);
   });
   char name[128];
+  const bool rhythm = argc > 2 && atoi(argv[2]) == 1;
+  if (rhythm) {
+    // the eval's rhythm: compute between store bursts, occupancy caps
+    for (long N : {256L, 512L}) {
+      const long P = N * N;
+      const long S = bytes / (16 * P);
+      const long wrote = S * 16 * P;
+      for (int G : {4, 64}) {
+        const long n_sc = (S + 16 * G - 1) / (16 * G);
+        for (int sl : {0, 4, 16, 48, 128})
+          for (int bar : {0, 1}) {
+            const long n_pb = P / 1024;
+            snprintf(name, sizeof name, "lds16-like %ld^2 g%-2d sleep%-3d bar%d", N, G, sl, bar);
+            time(name, wrote, [&] {
+              hipLaunchKernelGGL((contig_t<16, 1024>), dim3((unsigned)(n_pb * n_sc)), dim3(1024),
+                                 131584, 0, out, P, S, n_pb, n_sc, G, 0, sl, bar);
+            });
+          }
+        // register tile at 2 workgroups (8 waves) per CU: ~64 KiB LDS each
+        for (int sl : {0, 4, 16, 48, 128})
+          for (int lds : {0, 65536}) {
+            const long n_pb = P / 256;
+            const int lb = N == 512 ? 3 : 0, xi = N == 512 ? 1 : 0;
+            snprintf(name, sizeof name, "tile-like  %ld^2 g%-2d sleep%-3d lds%d", N, G, sl, lds);
+            time(name, wrote, [&] {
+              hipLaunchKernelGGL(rows4_t<4>, dim3((unsigned)(n_pb * n_sc)), dim3(256), lds, 0,
+                                 out, P, S, n_pb, n_sc, G, lb, xi, sl);
+            });
+          }
+      }
+    }
+    (void)hipFree(out);
+    return 0;
+  }
   for (long N : {256L, 512L}) {
     const long P = N * N;
     const long S = bytes / (16 * P);
