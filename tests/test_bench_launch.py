@@ -156,3 +156,44 @@ def test_pick_schedule_defaults():
     assert g["reserve_cus"] == 0
     c = bench.pick_schedule(argparse.Namespace(**dict(base, chunks=4)), 20, 100)
     assert (c["time_chunks"], c["reserve_cus"], c["fit_on_reserved"]) == (4, 16, True)
+
+
+def test_profile_tables_report_only_the_loaded_library(tmp_path, monkeypatch):
+    """bench._profile_entry hands out a PMC table entry only when its
+    library_sha16 is the library this process loads; an entry taken on
+    another build (or with no identity, as before round 5) is withheld and
+    named in STALE_COUNTERS."""
+    import json as _json
+    sys.path.insert(0, REPO)
+    import bench
+    from ska_sdp_screen_fitting_amd import _lib
+    (tmp_path / "profiles").mkdir()
+    tab = {"entries": [
+        {"workload": "config4", "eval_kernel": "k", "library_sha16": "aaaa", "v": 1},
+        {"workload": "config5", "eval_kernel": "k", "library_sha16": "bbbb", "v": 2},
+        {"workload": "config3", "eval_kernel": "k", "v": 3}]}
+    (tmp_path / "profiles" / "t.json").write_text(_json.dumps(tab))
+    monkeypatch.setattr(bench, "REPO", str(tmp_path))
+    monkeypatch.setattr(_lib, "library_identity", lambda path=None: {"sha16": "aaaa", "bytes": 1})
+    bench.STALE_COUNTERS.clear()
+    assert bench._profile_entry("t.json", "config4", "k")["v"] == 1
+    assert bench._profile_entry("t.json", "config5", "k") is None
+    assert bench._profile_entry("t.json", "config3", "k") is None
+    assert bench._profile_entry("t.json", "config9", "k") is None
+    assert bench.STALE_COUNTERS == {"t.json:config5:k": "bbbb", "t.json:config3:k": None}
+
+
+def test_committed_tables_carry_library_identity():
+    """Every entry the default line and its legs look up (config 4, config 5,
+    config-3 gain) carries the identity of the library it was taken on, and
+    the fit entries carry trace durations."""
+    import json as _json
+    for name in ("traffic.json", "mfma.json", "fit_flops.json"):
+        tab = _json.load(open(os.path.join(REPO, "profiles", name)))
+        keyed = {e["workload"]: e for e in tab["entries"] if e.get("library_sha16")}
+        for w in ("config4", "config5", "config3-gain"):
+            assert w in keyed, (name, w)
+        if name == "fit_flops.json":
+            for w in ("config4", "config5", "config3-gain"):
+                ks = keyed[w]["kernels"]
+                assert ks["kl_fit_pass_kernel"]["avg_ms"] is not None
