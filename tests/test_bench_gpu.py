@@ -17,6 +17,10 @@ def _bench(*args):
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--workload", "tiny",
            "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-side-legs",
            "--no-fits", "--no-child-legs", *args]
+    if "--parity" in args:
+        cmd.remove("--parity")
+    else:
+        cmd.append("--no-parity")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=REPO)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
@@ -40,3 +44,21 @@ def test_two_coefficient_sets_schedule(screen):
     # the default picks two sets for multi-step gain runs, one for phase
     default = _bench(*extra)
     assert default["config"]["schedule"]["coef_sets"] == (2 if screen == "gain" else 1)
+
+
+@pytest.mark.gpu
+def test_bench_line_carries_parity():
+    """The parity object every bench line carries (tools/bench_parity.py):
+    the fit of the fixture and of the reference-run synthetic sets, the
+    17^2 evaluations and the config-1 / config-2 cubes (made here, the FITS
+    legs being off) against the reference's own outputs -- all ok, and the
+    process exits 0."""
+    line = _bench("--parity")
+    par = line["parity"]
+    assert par["all_ok"], par
+    for k in ("fit_config2", "fit_synth20", "fit_synth50", "eval17", "config1", "config2"):
+        assert par[k]["ok"], (k, par[k])
+    assert par["fit_synth20"]["orders_equal"] and par["fit_synth50"]["flags_equal"]
+    assert par["config1"]["screens_png"]["mismatched_tessellated"] == 0
+    assert par["config2"]["cube_from"].startswith("make_aterm_image")
+    assert line["library"]["sha16"]
