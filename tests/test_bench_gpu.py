@@ -56,7 +56,8 @@ def test_bench_line_carries_parity():
     line = _bench("--parity")
     par = line["parity"]
     assert par["all_ok"], par
-    for k in ("fit_config2", "fit_synth20", "fit_synth50", "eval17", "config1", "config2"):
+    for k in ("fit_config2", "fit_synth20", "fit_synth50", "eval17", "config1", "config2",
+              "fit_amplitude_gain12", "fit_tec14", "gain_cube"):
         assert par[k]["ok"], (k, par[k])
     assert par["fit_synth20"]["orders_equal"] and par["fit_synth50"]["flags_equal"]
     assert par["config1"]["screens_png"]["mismatched_tessellated"] == 0

@@ -34,6 +34,16 @@ Checks (each reported as ``{max_err, tol, ok, ...}``):
   with abs(): 1e-1 at the patch pixels), the reference's evaluated planes at
   (t 4:6; f, station (3, 7), (9, 44)) within 1e-6, planes 2 / 3 equal to
   0 / 1, and the header cards.
+* ``fit_amplitude_gain12`` / ``fit_tec14``: the other soltab types of
+  ``stationscreen.run`` against the reference's own fits of them
+  (make_golden_gain.py / make_golden_tec.py): the log10-amplitude fit as
+  KLScreen.fit calls it (kl_screen.py:96-125: niter 3, the block-coupled
+  outlier sigma Q6, both pols) and the tec fit with the reference station and
+  with ref_ant = -1 (the precedence quirk Q15); same criteria as the phase fit.
+* ``gain_cube``: make_aterm_image on the gain solution set ("gain000" ->
+  phase000 + amplitude000: both fits, Screen.interpolate, the three-screen
+  evaluation with 10 **, kl_screen.py:319-378) vs the reference's
+  make_matrix planes, |d| <= 2e-6 x max(1, |value|).
 """
 
 import json
@@ -98,6 +108,101 @@ def fit_check(ctx, torch, dev, name):
                   slots=int(T * F * A), n_dir=int(D),
                   flagged_entries=int((g["w_out"] == 0).sum()),
                   adapted_orders=int(len(np.unique(g["orders"]))))
+
+
+def _fit_entry(got, want, tol=FIT_TOL):
+    """(coef, resid, w_out, orders) vs the reference's."""
+    coef, resid, w_out, orders = got
+    wc, wr, ww, wo = want
+    scale = max(1.0, float(np.abs(wc).max()))
+    cerr = float(np.abs(coef - wc).max()) / scale
+    rerr = float(np.abs(resid - wr).max())
+    return dict(cerr=cerr, rerr=rerr, orders_equal=bool(np.array_equal(orders, wo)),
+                flags_equal=bool(np.array_equal(w_out.view(np.uint32),
+                                                np.ascontiguousarray(ww).view(np.uint32))))
+
+
+def _device_fit(ctx, torch, dev, val, weight, st, **kw):
+    T, F, A, D = val.shape
+    v = torch.from_numpy(np.ascontiguousarray(val)).to(dev)
+    w = torch.from_numpy(np.ascontiguousarray(weight)).to(dev)
+    coef, resid = torch.zeros_like(v), torch.zeros_like(v)
+    w_out = torch.empty_like(w)
+    orders = torch.zeros((T, F, A), dtype=torch.int32, device=dev)
+    ctx.fit(v, w, T, F, A, st, coef=coef, resid=resid, w_out=w_out,
+            order_out=orders, **kw)
+    torch.cuda.synchronize(dev)
+    return (coef.cpu().numpy(), resid.cpu().numpy(), w_out.cpu().numpy(),
+            orders.cpu().numpy())
+
+
+def _merge(parts, **kw):
+    cerr = max(p["cerr"] for p in parts)
+    rerr = max(p["rerr"] for p in parts)
+    return _entry(max(cerr, rerr), FIT_TOL, coef_max_err_scaled=cerr, resid_max_err=rerr,
+                  orders_equal=all(p["orders_equal"] for p in parts),
+                  flags_equal=all(p["flags_equal"] for p in parts), **kw)
+
+
+def amplitude_check(ctx, torch, dev):
+    """The amplitude stationscreen.run of gain12 (both pols, niter 3, no
+    reference station, order min(12, max(3, round(D / 2))), kl_screen.py:
+    96-125) vs the reference's."""
+    from ska_sdp_screen_fitting_amd._lib import SF_SCREEN_AMPLITUDE
+    g = golden("gain12")
+    ctx.set_basis(g["piercepoints"])
+    T, F, A, D, P = g["amp_val"].shape
+    order = int(g["amp_order"])
+    parts = []
+    for p in range(P):
+        got = _device_fit(ctx, torch, dev, g["amp_val"][..., p], g["amp_weight"][..., p],
+                          [order] * A, screen_type=SF_SCREEN_AMPLITUDE, niter=3,
+                          nsigma=5.0, adjust_order=True, ref_ant=-1)
+        parts.append(_fit_entry(got, (g["amp_coef"][..., p], g["amp_resid"][..., p],
+                                      g["amp_w_out"][..., p], g["amp_orders"][..., p])))
+    return _merge(parts, slots=int(T * F * A * P), n_dir=int(D),
+                  flagged_entries=int((g["amp_w_out"] == 0).sum()))
+
+
+def tec_check(ctx, torch, dev):
+    """The tec stationscreen.run of tec14, with the reference station and
+    with ref_ant = -1 (quirk Q15), vs the reference's."""
+    from ska_sdp_screen_fitting_amd._lib import SF_SCREEN_TEC
+    from ska_sdp_screen_fitting_amd.stationscreen import station_orders
+    g = golden("tec14")
+    ctx.set_basis(g["piercepoints"])
+    parts = []
+    for case in ("ref", "noref"):
+        ref = int(g[f"{case}_ref_ant"])
+        st = station_orders(g["ant_pos"], ref, int(g["order"]))
+        got = _device_fit(ctx, torch, dev, g["val"], g["weight"], st,
+                          screen_type=SF_SCREEN_TEC, niter=int(g["niter"]), nsigma=5.0,
+                          adjust_order=True, ref_ant=ref)
+        parts.append(_fit_entry(got, tuple(g[f"{case}_{k}"] for k in
+                                           ("coef", "resid", "w_out", "orders"))))
+    T, F, A, D = g["val"].shape
+    return _merge(parts, slots=int(2 * T * F * A), n_dir=int(D), cases=["ref", "noref"])
+
+
+def gain_cube_check(outdir):
+    """make_aterm_image of the gain set (KL, 17^2) vs the reference's
+    make_matrix planes at its golden (freq, station) pairs."""
+    from ska_sdp_screen_fitting_amd import fits as sffits
+    from ska_sdp_screen_fitting_amd.make_aterm_images import make_aterm_image
+    g = golden("gain12")
+    outroot = os.path.join(outdir, "gain")
+    make_aterm_image(os.path.join(GOLDEN, "gain12.npz"), soltabname="gain000",
+                     screen_type="kl", outroot=outroot,
+                     bounds_deg=[124.565, 66.165, 127.895, 62.835],
+                     bounds_mid_deg=[126.23, 64.50], skymodel=None,
+                     padding_fraction=0, cellsize_deg=0.2, ncpu=0)
+    _, cube = sffits.read_cube(outroot + "_0.fits")
+    err = 0.0
+    for k, (f, a) in enumerate(g["pairs"]):
+        ref = g["gain17"][k]
+        err = max(err, float((np.abs(cube[:, f, a] - ref) / np.maximum(1.0, np.abs(ref))).max()))
+    return _entry(err, EVAL_TOL_FAST, shape_ok=tuple(cube.shape) == (8, 3, 5, 4, 17, 17),
+                  pairs=[[int(v) for v in fa] for fa in g["pairs"]])
 
 
 def eval17_check(ctx, torch, dev, flags):
@@ -285,6 +390,10 @@ def run(device, flags, cube_dirs=None):
         for key, name in FIT_SETS.items():
             res[key] = fit_check(ctx, torch, dev, name)
         res["eval17"] = eval17_check(ctx, torch, dev, flags)
+        res["fit_amplitude_gain12"] = amplitude_check(ctx, torch, dev)
+        res["fit_tec14"] = tec_check(ctx, torch, dev)
+        with tempfile.TemporaryDirectory() as tmp:
+            res["gain_cube"] = gain_cube_check(tmp)
         for name in ("config1", "config2"):
             d = (cube_dirs or {}).get(name)
             if d is not None:
