@@ -1571,6 +1571,9 @@ def main():
         if h is not None:
             ctx.stream_destroy(h)
     if dist.is_initialized():
+        # every rank waits for rank 0's line (parity included) before the
+        # group goes away
+        dist.barrier()
         dist.destroy_process_group()
     if parity_failed:
         log("PARITY FAILED: see the line's 'parity' object")
