@@ -1224,17 +1224,20 @@ def main():
         # reference station, 3 iterations (kl_screen.py:96-125)
         make_amplitudes(sol)
         order_amp = min(12, max(3, int(np.round(D / 2))))
-        amp = {"order": order_amp, "val": [], "w": [], "coef": [], "resid": [],
-               "w_out": [], "orders": []}
-        for p in range(2):
-            v = torch.from_numpy(np.ascontiguousarray(sol.amp_val[..., p])).to(dev)
-            w = torch.from_numpy(np.ascontiguousarray(sol.meta["amp_weight"][..., p])).to(dev)
-            amp["val"].append(v)
-            amp["w"].append(w)
-            amp["coef"].append(torch.empty_like(v))
-            amp["resid"].append(torch.empty_like(v))
-            amp["w_out"].append(torch.empty_like(w))
-            amp["orders"].append(torch.empty((T, F, A), dtype=torch.int32, device=dev))
+        # the two pols stacked along the station axis, one fit call for both
+        # (as stationscreen.run does: amplitudes are never referenced and
+        # their outlier sigma is per (station, freq) block, so the pols are
+        # independent blocks); the evaluation takes each pol's coefficients
+        # as its own contiguous [S][D] array (copied per step, 2 x 16 MB)
+        v = np.concatenate([sol.amp_val[..., p] for p in range(2)], axis=2)
+        w = np.concatenate([sol.meta["amp_weight"][..., p] for p in range(2)], axis=2)
+        v = torch.from_numpy(np.ascontiguousarray(v)).to(dev)
+        w = torch.from_numpy(np.ascontiguousarray(w)).to(dev)
+        amp = {"order": order_amp, "val": v, "w": w, "stacked": torch.empty_like(v),
+               "resid": torch.empty_like(v), "w_out": torch.empty_like(w),
+               "orders": torch.empty((T, F, 2 * A), dtype=torch.int32, device=dev),
+               "coef": [torch.empty((T, F, A, D), dtype=torch.float64, device=dev)
+                        for _ in range(2)]}
 
     # time chunks (the solution layout is time-major, so a chunk is a
     # contiguous slice of every array); phase slots are independent, so the
@@ -1243,8 +1246,11 @@ def main():
     sched = pick_schedule(args, D, T)
     n_chunks, n_sets = sched["time_chunks"], sched["coef_sets"]
     coef_sets = [coef] + [torch.empty_like(coef) for _ in range(n_sets - 1)]
-    amp_sets = ([amp["coef"]] + [[torch.empty_like(x) for x in amp["coef"]]
-                                 for _ in range(n_sets - 1)]) if gain else None
+    # per coefficient set: the stacked fit output and its per-pol copies
+    amp_sets = ([(amp["stacked"], amp["coef"])]
+                + [(torch.empty_like(amp["stacked"]),
+                    [torch.empty_like(x) for x in amp["coef"]])
+                   for _ in range(n_sets - 1)]) if gain else None
     pipelined = sched["pipelined"]
     bounds = [(T * c // n_chunks, T * (c + 1) // n_chunks) for c in range(n_chunks)]
     # the eval saturates HBM without every CU: its stream leaves
@@ -1292,13 +1298,23 @@ def main():
                 order_out=order_out[t0:t1], ant_offset=setup["ant_offset"],
                 ref_phase=refph[t0:t1])
         if gain:
-            for p in range(2):
-                ctx.fit(amp["val"][p][t0:t1], amp["w"][p][t0:t1], t1 - t0, F, A,
-                        [amp["order"]] * A, screen_type=SF_SCREEN_AMPLITUDE,
-                        niter=3, nsigma=5.0, adjust_order=True, ref_ant=-1,
-                        coef=amp_sets[b][p][t0:t1], resid=amp["resid"][p][t0:t1],
-                        w_out=amp["w_out"][p][t0:t1],
-                        order_out=amp["orders"][p][t0:t1])
+            ctx.fit(amp["val"][t0:t1], amp["w"][t0:t1], t1 - t0, F, 2 * A,
+                    [amp["order"]] * (2 * A), screen_type=SF_SCREEN_AMPLITUDE,
+                    niter=3, nsigma=5.0, adjust_order=True, ref_ant=-1,
+                    coef=amp_sets[b][0][t0:t1], resid=amp["resid"][t0:t1],
+                    w_out=amp["w_out"][t0:t1], order_out=amp["orders"][t0:t1])
+
+    def stage_amp(c, b=0):
+        """Gain: each pol's coefficients of the stacked amplitude fit into its
+        own contiguous array, on the eval stream after fit(c) (outside the
+        eval kernel's event window)."""
+        if not gain:
+            return
+        t0, t1 = bounds[c]
+        stacked, (xx, yy) = amp_sets[b]
+        with torch.cuda.stream(stream):
+            xx[t0:t1].copy_(stacked[t0:t1, :, :A])
+            yy[t0:t1].copy_(stacked[t0:t1, :, A:])
 
     def evaluate(c, b=0):
         t0, t1 = bounds[c]
@@ -1307,8 +1323,9 @@ def main():
         coef = coef_sets[b]
         cxx = cyy = None
         if gain:
-            cxx = amp_sets[b][0][t0:t1].reshape(-1, D)
-            cyy = amp_sets[b][1][t0:t1].reshape(-1, D)
+            xx, yy = amp_sets[b][1]
+            cxx = xx[t0:t1].reshape(-1, D)
+            cyy = yy[t0:t1].reshape(-1, D)
         if checksum:
             ctx.eval_sums(coef[t0:t1].reshape(-1, D), n, out,
                           slot_sums[t0 * F * A:t1 * F * A], ring, coef_xx=cxx,
@@ -1350,6 +1367,7 @@ def main():
         issue_fit(0)
         for i, (k, c) in enumerate(items):
             stream.wait_event(fit_done[i][1])
+            stage_amp(c, k % n_sets)
             e2 = torch.cuda.Event(enable_timing=True)
             e3 = torch.cuda.Event(enable_timing=True)
             e2.record(stream)

@@ -126,12 +126,30 @@ def run(soltab, outsoltab, order=12, beta=5.0 / 3.0, niter=2, nsigma=5.0,
     resid = np.zeros(val.shape)
     w_out = np.zeros(weight.shape, dtype=np.float32)
     orders = np.zeros((n_times, n_freqs, n_stations, n_pols))
-    for pol in range(n_pols):
-        c, r, w, o = _device_fit(val[..., pol], weight[..., pol], pp, st_order,
-                                 stype, niter, nsigma, adjust_order, ref_ant,
-                                 beta, r_0, device)
-        coef[..., pol], resid[..., pol], w_out[..., pol] = c, r, w
-        orders[..., pol] = o
+    if stype == SF_SCREEN_AMPLITUDE and n_pols > 1:
+        # amplitude screens are never referenced (stationscreen.py:994 applies
+        # to phase / tec) and their outlier sigma is per (station, freq) block
+        # (Q6): the pols are independent station blocks, so ONE fit of the
+        # pols stacked along the station axis gives every pol's result bit
+        # for bit, with the fixed per-call costs (host syncs, mask table,
+        # latency-bound subset bases -- shared when the pols' flags agree)
+        # paid once (tests/test_gain.py::test_stacked_pol_fit_equals_per_pol)
+        c, r, w, o = _device_fit(
+            np.concatenate([val[..., p] for p in range(n_pols)], axis=2),
+            np.concatenate([weight[..., p] for p in range(n_pols)], axis=2),
+            pp, np.tile(st_order, n_pols), stype, niter, nsigma, adjust_order,
+            -1, beta, r_0, device)
+        for pol in range(n_pols):
+            sl = slice(pol * n_stations, (pol + 1) * n_stations)
+            coef[..., pol], resid[..., pol], w_out[..., pol] = c[:, :, sl], r[:, :, sl], w[:, :, sl]
+            orders[..., pol] = o[:, :, sl]
+    else:
+        for pol in range(n_pols):
+            c, r, w, o = _device_fit(val[..., pol], weight[..., pol], pp, st_order,
+                                     stype, niter, nsigma, adjust_order, ref_ant,
+                                     beta, r_0, device)
+            coef[..., pol], resid[..., pol], w_out[..., pol] = c, r, w
+            orders[..., pol] = o
 
     times, freqs = np.asarray(soltab.time), np.asarray(soltab.freq)
     axes = ["time", "freq", "ant", "dir"]

@@ -324,3 +324,47 @@ def test_tess_gain_vs_oracle(gain, smooth):
         want = ov.smooth(want, smooth)
     np.testing.assert_allclose(out.cpu().numpy(), want, rtol=0,
                                atol=1e-6 * max(1.0, np.abs(want).max()))
+
+
+@pytest.mark.gpu
+def test_stacked_pol_fit_equals_per_pol(gain):
+    """stationscreen.run fits the amplitude pols in ONE sf_kl_fit call,
+    stacked along the station axis (amplitudes are never referenced and
+    their outlier sigma is per (station, freq) block, Q6): bit for bit the
+    per-pol fits -- on the reference's gain set and on a larger synthetic
+    one with NaN / all-flagged blocks and different flags per pol."""
+    from ska_sdp_screen_fitting_amd import geometry
+    from ska_sdp_screen_fitting_amd._lib import SF_SCREEN_AMPLITUDE
+    from ska_sdp_screen_fitting_amd.synthetic import make_amplitudes, make_solutions
+    torch, dev = _torch_dev()
+    ctx = _ctx(torch, dev)
+    s = make_solutions(n_ant=6, n_time=5, n_freq=3, n_dir=20, seed=17)
+    make_amplitudes(s, seed=18, flag_frac=0.05, outlier_frac=0.03)
+    amp, wt = s.amp_val.copy(), s.meta["amp_weight"].copy()
+    amp[:, 1, 2, :, 0] = np.nan
+    wt[:, 0, 4, :, 1] = 0.0
+    wt[2, 2, 1, 3, 1] = 0.0  # the pols' flags differ
+    pp, _, _ = geometry.piercepoints(s.dir_radec)
+    for val, w, pp_, order in ((gain["amp_val"], gain["amp_weight"], gain["piercepoints"],
+                                int(gain["amp_order"])), (amp, wt, pp, 10)):
+        ctx.set_basis(pp_)
+        T, F, A, D, P = val.shape
+
+        def fit(v, ww, n_st):
+            v = torch.from_numpy(np.ascontiguousarray(v)).to(dev)
+            ww = torch.from_numpy(np.ascontiguousarray(ww)).to(dev)
+            out = (torch.zeros_like(v), torch.zeros_like(v), torch.empty_like(ww),
+                   torch.zeros((T, F, n_st), dtype=torch.int32, device=dev))
+            ctx.fit(v, ww, T, F, n_st, [order] * n_st, screen_type=SF_SCREEN_AMPLITUDE,
+                    niter=3, ref_ant=-1, coef=out[0], resid=out[1], w_out=out[2],
+                    order_out=out[3])
+            torch.cuda.synchronize()
+            return [x.cpu().numpy() for x in out]
+
+        stacked = fit(np.concatenate([val[..., p] for p in range(P)], axis=2),
+                      np.concatenate([w[..., p] for p in range(P)], axis=2), A * P)
+        for p in range(P):
+            single = fit(val[..., p], w[..., p], A)
+            for a, b in zip(single, stacked):
+                assert np.array_equal(a.view(np.uint8),
+                                      np.ascontiguousarray(b[:, :, p * A:(p + 1) * A]).view(np.uint8))
