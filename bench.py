@@ -825,14 +825,15 @@ def side_legs(ctx, torch, dev, stream, fit_stream, fit, evaluate, coef, bounds,
     return res
 
 
-def child_leg(extra, what, timeout_s=420):
+def child_leg(extra, what, timeout_s=420, side=False):
     """One workload of BASELINE.json beside the config-4 line, in a child
     ``bench.py`` (its own device buffers; the parent holds its own and is
-    idle meanwhile): its value, eval roofline, checks and wall time."""
+    idle meanwhile): its value, eval roofline, checks and wall time; with
+    ``side``, also the child's eval alone on the chip (its side leg)."""
     import subprocess
     cmd = [sys.executable, os.path.abspath(__file__), "--gpus", "1",
-           "--no-cpu-baseline", "--no-fits", "--no-side-legs", "--no-child-legs",
-           "--no-parity"] + extra
+           "--no-cpu-baseline", "--no-fits", "--no-child-legs",
+           "--no-parity"] + ([] if side else ["--no-side-legs"]) + extra
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     t0 = time.perf_counter()
     try:
@@ -858,6 +859,11 @@ def child_leg(extra, what, timeout_s=420):
     if sm:
         out.update(sampled_slots=sm, checksums_match=sm.get("checksums_match"),
                    max_abs_err_vs_fp64=sm["max_abs_err_vs_fp64"], ok=sm["ok"])
+    alone = (r.get("side_legs") or {}).get("eval_fp32_sincos")
+    if alone:
+        # the same eval with nothing beside it (the step overlaps the fit of
+        # the next step with it: DESIGN.md, gain screens)
+        out["eval_alone"] = {k: alone[k] for k in ("launch_ms", "achieved_GBs", "frac", "slots")}
     return out
 
 
@@ -883,7 +889,7 @@ def child_legs():
             "(bench.py --workload config5 --steps 1 --warmup 1)"),
         "gain_config3": child_leg(
             ["--screen", "gain", "--workload", "config3", "--steps", "30", "--warmup", "2"],
-            "gain screens on the config-3 shape in a child process"),
+            "gain screens on the config-3 shape in a child process", side=True),
         "tess_config3": child_leg(
             ["--screen", "tess", "--workload", "config3", "--steps", "10", "--warmup", "2"],
             "tessellated fill on the config-3 shape in a child process"),
