@@ -118,6 +118,15 @@ def parse():
     ap.add_argument("--eval-groups", type=int, default=0,
                     help="SF_OPT_EVAL_GROUPS: most 16-slot groups per eval work "
                          "item (0 = library default)")
+    ap.add_argument("--eval-kernel", type=int, default=0,
+                    help="SF_OPT_EVAL_KERNEL: 0 auto (default), else one of "
+                         "SF_EVAL_KERNEL_* (A/B runs)")
+    ap.add_argument("--eval-bands", type=int, default=0,
+                    help="SF_OPT_EVAL_BANDS: pixel bands of an eval launch "
+                         "(0 = library default)")
+    ap.add_argument("--eval-sleep", type=int, default=0,
+                    help="SF_OPT_EVAL_SLEEP: LDS-staged eval waves sleep n x 64 "
+                         "cycles before each group's barrier (diagnostic)")
     ap.add_argument("--checksum", default="auto", choices=("auto", "on", "off"),
                     help="per-slot output checksums (sf_kl_eval_sums); auto: on "
                          "for config4 / config5, whose cubes are discarded")
@@ -1166,8 +1175,11 @@ def main():
     from ska_sdp_screen_fitting_amd._lib import (SF_EVAL_FAST_SINCOS,
                                                  SF_EVAL_NAN_SCRUB,
                                                  SF_EVAL_NT_STORES,
+                                                 SF_OPT_EVAL_BANDS,
                                                  SF_OPT_EVAL_GROUPS,
                                                  SF_OPT_EVAL_INT,
+                                                 SF_OPT_EVAL_KERNEL,
+                                                 SF_OPT_EVAL_SLEEP,
                                                  SF_OPT_EVAL_XCD_MAP)
     from ska_sdp_screen_fitting_amd.distributed import setup_shard
     from ska_sdp_screen_fitting_amd._lib import SF_SCREEN_AMPLITUDE, library_identity
@@ -1287,6 +1299,9 @@ def main():
     ctx.set_option(SF_OPT_EVAL_XCD_MAP, args.eval_xcd_map)
     ctx.set_option(SF_OPT_EVAL_GROUPS, args.eval_groups)
     ctx.set_option(SF_OPT_EVAL_INT, args.eval_int)
+    ctx.set_option(SF_OPT_EVAL_KERNEL, args.eval_kernel)
+    ctx.set_option(SF_OPT_EVAL_BANDS, args.eval_bands)
+    ctx.set_option(SF_OPT_EVAL_SLEEP, args.eval_sleep)
     eval_kernel_name = ctx.eval_kernel(flags, gain=gain)
     contraction = ctx.eval_contraction(flags, gain=gain)
     # discard + checksum mode: the cubes go

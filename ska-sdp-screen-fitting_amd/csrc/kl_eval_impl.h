@@ -1007,12 +1007,19 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
       v4d acc[TPW];
 #pragma unroll
       for (int t = 0; t < TPW; ++t) acc[t] = v4d{a0, a0, a0, a0};
+      if constexpr (kEnergyDiag == 3) {
+        // energy diagnostic: no contraction (the LDS tile, barrier and
+        // stores stay)
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) acc[t] = v4d{af[0], af[0], bf[0][t], bf[0][t]};
+      } else {
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
         for (int t = 0; t < TPW; ++t)
           acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[kk], bf[kk][t],
                                                         acc[t], 0, 0, 0);
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float red[TPW];
@@ -1045,7 +1052,12 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             float sn, cs;
-            sincos_rev(rv[e], sn, cs);
+            if constexpr (kEnergyDiag == 3) {
+              sn = rv[e];  // energy diagnostic: no sincos
+              cs = -rv[e];
+            } else {
+              sincos_rev(rv[e], sn, cs);
+            }
             if (kBE) {
               cs = bswapf(cs);
               sn = bswapf(sn);

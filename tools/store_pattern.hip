@@ -20,6 +20,7 @@
 //   hipcc --offload-arch=gfx950 -O3 tools/store_pattern.hip -o tools/store_pattern
 //   tools/store_pattern [GiB [1]]   (1: the rhythm sweep -- s_sleep "compute"
 //   between store bursts, a barrier per group, LDS-capped occupancy)
+//   tools/store_pattern GiB 2 [R]   (2: long launches, R passes of the ring)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -61,7 +62,8 @@ __global__ __launch_bounds__(256) void lin(float* out, long n4) {
 // register tile: NW waves x 64 pixels per workgroup, G groups of 16 slots
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void rows4(float* out, long P, long S, long n_pb,
-                                                 long n_sc, int G, int lb, int xi) {
+                                                 long n_sc, int G, int lb, int xi,
+                                                 long ring) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   long pb, sc;
   item(blockIdx.x, n_pb, n_sc, lb, xi, pb, sc);
@@ -77,7 +79,7 @@ __global__ __launch_bounds__(64 * NW) void rows4(float* out, long P, long S, lon
       const long s = s0 + (l >> 4) + 4 * r;
       if (s < S) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) st(out + (s * 4 + q) * P + p0, v);
+        for (int q = 0; q < 4; ++q) st(out + ((s0 % ring + (s - s0)) * 4 + q) * P + p0, v);
       }
     }
   }
@@ -85,9 +87,10 @@ __global__ __launch_bounds__(64 * NW) void rows4(float* out, long P, long S, lon
 
 // LDS-staged pattern: a workgroup of NW waves owns RUN pixels; wave w writes
 // slots w * (16 / NW) + j of each group, 1 KiB per store instruction
-template <int NW, int RUN>
+template <int NW, int RUN, bool VAR = false>
 __global__ __launch_bounds__(64 * NW) void contig(float* out, long P, long S, long n_pb,
-                                                  long n_sc, int G, int lb, int xi) {
+                                                  long n_sc, int G, int lb, int xi,
+                                                  long ring) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   long pb, sc;
   item(blockIdx.x, n_pb, n_sc, lb, xi, pb, sc);
@@ -105,7 +108,13 @@ __global__ __launch_bounds__(64 * NW) void contig(float* out, long P, long S, lo
 #pragma unroll
         for (int c = 0; c < RUN / 256; ++c) {
           const long p = pix0 + c * 256 + 4 * l;
-          if (p < P) st(out + (s * 4 + q) * P + p, v);
+          if (p < P) {
+            // VAR: values that differ per pixel, slot and plane (the eval's)
+            const v4f u = VAR ? v4f{__builtin_sinf((float)(p + s)), __builtin_cosf((float)(p ^ s)),
+                                    (float)(q - p), (float)(s * 3 + c)}
+                              : v;
+            st(out + ((s0 % ring + (s - s0)) * 4 + q) * P + p, u);
+          }
         }
     }
   }
@@ -210,6 +219,58 @@ int main(int argc, char** argv) {
   });
   char name[128];
   const bool rhythm = argc > 2 && atoi(argv[2]) == 1;
+  if (argc > 2 && atoi(argv[2]) == 2) {
+    // long launches (round 5): the same orders over R passes of the ring in
+    // ONE launch (slot s -> s mod ring, as the eval's ring), 40-80 ms per
+    // launch instead of 2.5-3.5 ms, so the launch ramp is out of the number
+    const long R = argc > 3 ? atol(argv[3]) : 16;
+    for (long N : {256L, 512L}) {
+      const long P = N * N;
+      const long ring = bytes / (16 * P);  // a multiple of 16 slots
+      const long S = ring * R;
+      const long wrote = S * 16 * P;
+      for (int G : {1, 2, 4, 16, 64}) {
+        const long n_sc = (S + 16 * G - 1) / (16 * G);
+        for (int xi : {0, 1})
+          for (int lb : {0, 3}) {
+            const long n_pb = P / 256;
+            if (lb && (n_pb % (8 << lb))) continue;
+            if (N == 256 && lb) continue;
+            snprintf(name, sizeof name, "long rows4  %ld^2 nw4 g%-2d x%d b%d", N, G, xi, 1 << lb);
+            time(name, wrote, [&] {
+              hipLaunchKernelGGL(rows4<4>, dim3((unsigned)(n_pb * n_sc)), dim3(256), 0, 0, out,
+                                 P, S, n_pb, n_sc, G, lb, xi, ring);
+            });
+          }
+        if (G == 2 || G == 4)
+          for (int xi : {0, 1}) {
+            const long n_pb = P / 1024;
+            snprintf(name, sizeof name, "long contig %ld^2 run4096 g%-2d x%d VAR", N, G, xi);
+            time(name, wrote, [&] {
+              hipLaunchKernelGGL((contig<16, 1024, true>), dim3((unsigned)(n_pb * n_sc)),
+                                 dim3(1024), 0, 0, out, P, S, n_pb, n_sc, G, 0, xi, ring);
+            });
+          }
+        for (int shape : {0, 2})
+          for (int xi : {0, 1}) {
+            const int run = 256 << shape;
+            const long n_pb = P / run;
+            snprintf(name, sizeof name, "long contig %ld^2 run%-4d g%-2d x%d", N, run * 4, G, xi);
+            time(name, wrote, [&] {
+              const unsigned nb = (unsigned)(n_pb * n_sc);
+              if (shape == 0)
+                hipLaunchKernelGGL((contig<4, 256>), dim3(nb), dim3(256), 0, 0, out, P, S, n_pb,
+                                   n_sc, G, 0, xi, ring);
+              else
+                hipLaunchKernelGGL((contig<16, 1024>), dim3(nb), dim3(1024), 0, 0, out, P, S,
+                                   n_pb, n_sc, G, 0, xi, ring);
+            });
+          }
+      }
+    }
+    (void)hipFree(out);
+    return 0;
+  }
   if (rhythm) {
     // the eval's rhythm: compute between store bursts, occupancy caps
     for (long N : {256L, 512L}) {
@@ -260,10 +321,10 @@ int main(int argc, char** argv) {
             time(name, wrote, [&] {
               if (nw == 4)
                 hipLaunchKernelGGL(rows4<4>, dim3((unsigned)(n_pb * n_sc)), dim3(256), 0, 0,
-                                   out, P, S, n_pb, n_sc, G, lb, xi);
+                                   out, P, S, n_pb, n_sc, G, lb, xi, S);
               else
                 hipLaunchKernelGGL(rows4<8>, dim3((unsigned)(n_pb * n_sc)), dim3(512), 0, 0,
-                                   out, P, S, n_pb, n_sc, G, lb, xi);
+                                   out, P, S, n_pb, n_sc, G, lb, xi, S);
             });
           }
       }
@@ -280,13 +341,13 @@ int main(int argc, char** argv) {
             const unsigned nb = (unsigned)(n_pb * n_sc);
             if (shape == 0)
               hipLaunchKernelGGL((contig<4, 256>), dim3(nb), dim3(256), 0, 0, out, P, S, n_pb,
-                                 n_sc, G, 0, xi);
+                                 n_sc, G, 0, xi, S);
             else if (shape == 1)
               hipLaunchKernelGGL((contig<8, 512>), dim3(nb), dim3(512), 0, 0, out, P, S, n_pb,
-                                 n_sc, G, 0, xi);
+                                 n_sc, G, 0, xi, S);
             else
               hipLaunchKernelGGL((contig<16, 1024>), dim3(nb), dim3(1024), 0, 0, out, P, S,
-                                 n_pb, n_sc, G, 0, xi);
+                                 n_pb, n_sc, G, 0, xi, S);
           });
         }
       }
