@@ -776,11 +776,13 @@ def mfma_line(kernel, launch_slots, P, D, launch_s, workload, n_contract=1,
 
 
 def side_legs(ctx, torch, dev, stream, fit_stream, fit, evaluate, coef, bounds,
-              F, A, D, P, out, ring, flags, gain=False, amp=None):
+              F, A, D, P, out, ring, flags, gain=False, amp=None, fit_ones=None):
     """Untimed side measurements after the timed steps: (1) the evaluation of
     time chunk 0 with the fp64 sincos epilogue (--precise-sincos) beside the
-    default fp32 one, (2) the fit of chunk 0 alone on the whole chip.  HIP
-    events on the stream each runs on."""
+    default fp32 one, (2) the fit of chunk 0 alone on the whole chip, with the
+    workload's weights and ("also report an all-ones
+    variant") with every weight 1 -- run first, so that the outputs left
+    behind are the workload's.  HIP events on the stream each runs on."""
     from ska_sdp_screen_fitting_amd._lib import SF_EVAL_FAST_SINCOS
     t0, t1 = bounds[0]
     n = (t1 - t0) * F * A
@@ -815,6 +817,13 @@ def side_legs(ctx, torch, dev, stream, fit_stream, fit, evaluate, coef, bounds,
         res[name] = {"kernel": ctx.eval_kernel(fl, gain=gain), "slots": n,
                      "launch_ms": ms, "slots_per_s": n / ms * 1e3,
                      "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS}
+    if fit_ones is not None:
+        ms = timed(lambda: fit_ones(fit_stream), fit_stream)
+        res["fit_alone_all_ones_weights"] = {
+            "slots": n, "ms": ms, "slots_per_s": n / ms * 1e3,
+            "n_masks": ctx.fit_stats().get("n_masks"),
+            "what": "the fit of chunk 0 with every weight 1 (no flagged "
+                    "directions; the outliers stay in the phases)"}
     ms = timed(lambda: fit(0, fit_stream), fit_stream)
     res["fit_alone_whole_chip"] = {"slots": n, "ms": ms,
                                    "slots_per_s": n / ms * 1e3}
@@ -1310,10 +1319,11 @@ def main():
                                          and args.workload in ("config4", "config5"))
     slot_sums = torch.zeros(S, dtype=torch.int32, device=dev) if checksum else None
 
-    def fit(c, fs, b=0):
+    def fit(c, fs, b=0, wts=None):
         t0, t1 = bounds[c]
         ctx.set_stream(fs.cuda_stream)
-        ctx.fit(phase[t0:t1], weight[t0:t1], t1 - t0, F, A, setup["st_order"],
+        w_in = weight if wts is None else wts
+        ctx.fit(phase[t0:t1], w_in[t0:t1], t1 - t0, F, A, setup["st_order"],
                 niter=2, nsigma=5.0, adjust_order=True, ref_ant=setup["ref_ant"],
                 coef=coef_sets[b][t0:t1], resid=resid[t0:t1], w_out=w_out[t0:t1],
                 order_out=order_out[t0:t1], ant_offset=setup["ant_offset"],
@@ -1460,8 +1470,11 @@ def main():
     side = {}
     if not args.no_side_legs and not args.eval_only:
         log("side legs")
+        ones = torch.ones_like(weight)
         side = side_legs(ctx, torch, dev, stream, first_fit_stream, fit, evaluate,
-                         coef, bounds, F, A, D, P, out, ring, flags, gain, amp)
+                         coef, bounds, F, A, D, P, out, ring, flags, gain, amp,
+                         fit_ones=lambda fs: fit(0, fs, 0, ones))
+        del ones
     if (rank == 0 and world == 1 and args.workload == "config4" and not gain
             and not args.no_child_legs and not args.as_shard_of
             and not args.eval_only):
