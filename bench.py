@@ -287,10 +287,12 @@ def _cpu_worker(job):
     (phi, w, order, pp, cpix_args, n_eval) = job
     basis = okl.Basis(pp)
     t0 = time.perf_counter()
-    coefs = []
+    coefs, w_outs, orders = [], [], []
     for k in range(phi.shape[0]):
-        white, _, _, _, _ = okl.fit_slot(phi[k], w[k], order[k], order[k], basis)
+        white, _, w_o, o, _ = okl.fit_slot(phi[k], w[k], order[k], order[k], basis)
         coefs.append(white)
+        w_outs.append(w_o)
+        orders.append(o)
     t_fit = time.perf_counter() - t0
     x, y = cpix_args
     cpix = okl.cpix_matrix(pp, x, y)
@@ -301,21 +303,43 @@ def _cpu_worker(job):
         planes = okl.eval_planes(ph).astype(np.float32)
         del planes
     t_eval = time.perf_counter() - t0
-    return phi.shape[0], t_fit, n_eval, t_eval
+    # the sample's fit outputs go back to the parent as the checker of the
+    # GPU's fit of the same slots (_oracle_sample_check)
+    return (phi.shape[0], t_fit, n_eval, t_eval,
+            (coefs, np.array(w_outs, np.float32), np.array(orders)))
+
+
+def baseline_sample(sol, setup, n_workers, slots_fit=64):
+    """The CPU baseline's fit sample: per worker k, slots_fit random times
+    of station k (skipping the reference station) at freq k mod F."""
+    T, F, A, D = sol.val.shape
+    ref = setup["ref_ant"]
+    rng = np.random.default_rng(1)
+    where = []
+    for k in range(n_workers):
+        a = [a for a in range(A) if a != ref][k % (A - 1)]
+        ts = rng.choice(T, size=min(slots_fit, T), replace=False)
+        where.append((ts, k % F, a))
+    return where
+
+
+def gpu_sample_outputs(torch, where, coef, w_out, order_out):
+    """The GPU fit's outputs at the baseline sample's slots (host copies)."""
+    out = []
+    for ts, f, a in where:
+        ti = torch.as_tensor(ts, device=coef.device)
+        out.append((coef[ti, f, a].cpu().numpy(), w_out[ti, f, a].cpu().numpy(),
+                    order_out[ti, f, a].cpu().numpy()))
+    return out
 
 
 def cpu_baseline(sol, setup, n_workers, rule="", slots_fit=64, slots_eval=192):
     import multiprocessing as mp
 
-    T, F, A, D = sol.val.shape
-    ref = setup["ref_ant"]
     phi = sol.val - setup["ref_phase"].cpu().numpy()[:, :, None, :]
     jobs = []
-    rng = np.random.default_rng(1)
-    for k in range(n_workers):
-        a = [a for a in range(A) if a != ref][k % (A - 1)]
-        ts = rng.choice(T, size=min(slots_fit, T), replace=False)
-        f = k % F
+    where = baseline_sample(sol, setup, n_workers, slots_fit)
+    for ts, f, a in where:
         jobs.append((phi[ts, f, a], sol.weight[ts, f, a],
                      [setup["st_order"][a]] * len(ts), setup["piercepoints"],
                      (setup["x"], setup["y"]), slots_eval))
@@ -341,6 +365,7 @@ def cpu_baseline(sol, setup, n_workers, rule="", slots_fit=64, slots_eval=192):
     t_ev = sum(r[3] for r in res)
     per_slot = t_fit / n_fit + t_ev / n_ev  # core-seconds per slot (fit + eval)
     P = len(setup["x"]) * len(setup["y"])
+    samples = [(wh, r[4]) for wh, r in zip(where, res)]
     # the reference itself, timed during the survey on an 8-vCPU Xeon
     # (SURVEY.md §6): calculate_kl_screen 8.5 us / pixel / slot / core,
     # _fit_screen 68-92 us / slot (unflagged)
@@ -366,7 +391,56 @@ def cpu_baseline(sol, setup, n_workers, rule="", slots_fit=64, slots_eval=192):
             "ref_s_per_slot_core": ref_slot_s,
             "ref_slots_per_s_at_cores": n_workers / ref_slot_s,
         },
+        "_samples": samples,
     }
+
+
+def _oracle_sample_check(samples, gpu, pp):
+    """The CPU baseline's oracle fits (stationscreen.py:597-782 restated,
+    oracle/kl.py fit_slot) as the checker of the GPU's fit of the same slots
+    of the benchmarked workload (``gpu``: gpu_sample_outputs, taken right
+    after the timed steps and side legs, before the parity legs move the
+    shared context to other bases): orders and flagged weights bit-equal,
+    coefficients <= 1e-8 x max(1, |coef|max) -- the GPU tests' criterion,
+    where a slot over it counts as explained only when its order-K normal
+    matrix U_k^T W U_k has a singular value <= 1e-3 (the reference's pinv
+    cutoff: its own output is chaotic there, tests/test_oracle_golden.py
+    ill_conditioned_slots)."""
+    sys.path.insert(0, REPO)
+    from oracle import kl as okl  # test infrastructure: the baseline leg's checker
+
+    n = n_ord = n_w = 0
+    err_max = 0.0
+    over = []
+    scale = 1.0
+    for g_c, _, _ in gpu:
+        scale = max(scale, float(np.nanmax(np.abs(g_c))))
+    for (_, (wh, wo, od)), (g_c, g_w, g_o) in zip(samples, gpu):
+        wh = np.asarray(wh)
+        n += len(g_o)
+        n_ord += int((g_o != od.astype(g_o.dtype)).sum())
+        n_w += int((g_w != wo).sum(axis=-1).astype(bool).sum())
+        err = np.abs(g_c - wh).max(axis=-1)
+        err_max = max(err_max, float(np.nanmax(err)))
+        for k in np.where(~(err <= 1e-8 * scale))[0]:
+            over.append((wo[k], int(od[k])))
+    basis = okl.Basis(pp)
+    unexplained = 0
+    for w, o in over:
+        unfl = np.where(w > 0)[0]
+        _, _, u = okl.calculate_svd(basis.pp[unfl], 100.0, 5.0 / 3.0)
+        wd = np.diag(w[unfl].astype(np.float64))
+        sv = np.linalg.svd(u[:, :o].T @ (wd @ u)[:, :o], compute_uv=False)
+        if o == 0 or sv.min() > 1e-3:
+            unexplained += 1
+    ok = n_ord == 0 and n_w == 0 and unexplained == 0
+    return {"slots": n, "orders_differ": n_ord, "weight_rows_differ": n_w,
+            "coef_max_abs_err": err_max, "coef_scale": scale, "tol": 1e-8 * scale,
+            "slots_over_tol": len(over), "over_tol_unexplained": unexplained,
+            "ok": ok,
+            "what": "the GPU fit of the benchmarked workload vs the oracle "
+                    "(oracle/kl.py fit_slot, pinned to the reference's outputs) "
+                    "on the CPU baseline's sampled slots"}
 
 
 def _affinity():
@@ -1475,6 +1549,20 @@ def main():
                          coef, bounds, F, A, D, P, out, ring, flags, gain, amp,
                          fit_ones=lambda fs: fit(0, fs, 0, ones))
         del ones
+    # the CPU baseline's sample of this workload's fit, taken now: the
+    # parity and FITS legs below reuse this process's context with other
+    # bases and grids
+    gpu_sample = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.eval_only:
+        nw_cpu, rule_cpu = cpu_share()
+        if args.cpu_workers:
+            nw_cpu, rule_cpu = args.cpu_workers, "--cpu-workers"
+        nw_cpu = max(1, nw_cpu)
+        for c in range(n_chunks):
+            fit(c, stream, 0)
+        torch.cuda.synchronize(dev)
+        gpu_sample = gpu_sample_outputs(torch, baseline_sample(sol, setup, nw_cpu),
+                                        coef_sets[0], w_out, order_out)
     if (rank == 0 and world == 1 and args.workload == "config4" and not gain
             and not args.no_child_legs and not args.as_shard_of
             and not args.eval_only):
@@ -1605,6 +1693,16 @@ def main():
             if args.cpu_workers:
                 nw, rule = args.cpu_workers, "--cpu-workers"
             line["cpu_baseline"] = cpu_baseline(sol, setup, max(1, nw), rule)
+            samples = line["cpu_baseline"].pop("_samples")
+            if gpu_sample is not None:
+                chk = _oracle_sample_check(samples, gpu_sample, setup["piercepoints"])
+                line["cpu_baseline"]["oracle_check"] = chk
+                line.setdefault("parity", {})["fit_oracle_sample"] = {
+                    "max_err": chk["coef_max_abs_err"], "tol": chk["tol"],
+                    "ok": chk["ok"], "slots": chk["slots"]}
+                if "all_ok" in line["parity"]:
+                    line["parity"]["all_ok"] = line["parity"]["all_ok"] and chk["ok"]
+                parity_failed = parity_failed or not chk["ok"]
             # BASELINE.json configs[0] / [1]: the CPU path of make_aterm_image
             # on one core, next to fits_wallclock.config1 / config2
             legs = cpu_reference_path()

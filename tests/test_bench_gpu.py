@@ -17,6 +17,9 @@ def _bench(*args):
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--workload", "tiny",
            "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-side-legs",
            "--no-fits", "--no-child-legs", *args]
+    if "--cpu-baseline" in args:
+        cmd.remove("--cpu-baseline")
+        cmd.remove("--no-cpu-baseline")
     if "--parity" in args:
         cmd.remove("--parity")
     else:
@@ -63,3 +66,17 @@ def test_bench_line_carries_parity():
     assert par["config1"]["screens_png"]["mismatched_tessellated"] == 0
     assert par["config2"]["cube_from"].startswith("make_aterm_image")
     assert line["library"]["sha16"]
+
+
+@pytest.mark.gpu
+def test_cpu_baseline_leg_checks_the_fit_on_its_sample():
+    """The CPU baseline leg's oracle fits (the sample it times) check the
+    GPU's fit of the same slots of the benchmarked workload: orders and
+    flags equal, coefficients within 1e-8 -- in the line as
+    cpu_baseline.oracle_check and parity.fit_oracle_sample."""
+    line = _bench("--cpu-baseline", "--cpu-workers", "4")
+    chk = line["cpu_baseline"]["oracle_check"]
+    assert chk["ok"], chk
+    assert chk["slots"] >= 16 and chk["orders_differ"] == 0
+    assert line["parity"]["fit_oracle_sample"]["ok"]
+    assert "_samples" not in line["cpu_baseline"]

@@ -197,3 +197,70 @@ def test_committed_tables_carry_library_identity():
             for w in ("config4", "config5", "config3-gain"):
                 ks = keyed[w]["kernels"]
                 assert ks["kl_fit_pass_kernel"]["avg_ms"] is not None
+
+
+def test_oracle_sample_check_flags_mismatches():
+    """bench._oracle_sample_check (the CPU baseline leg's oracle fits as the
+    checker of the GPU's fit of the same slots): equal outputs pass; a
+    changed order, a changed flag or a coefficient off by more than the
+    tolerance at a well-conditioned slot fail."""
+    import numpy as np
+
+    import bench
+    from oracle import kl as okl
+    from ska_sdp_screen_fitting_amd import geometry
+    from ska_sdp_screen_fitting_amd.synthetic import make_solutions
+
+    T, F, A, D = 6, 1, 3, 8
+    s = make_solutions(n_ant=A, n_time=T, n_freq=F, n_dir=D)
+    pp = geometry.piercepoints(s.dir_radec)[0]
+    basis = okl.Basis(pp)
+    coef = np.zeros((T, F, A, D))
+    w_out = s.weight.astype(np.float32).copy()
+    order_out = np.zeros((T, F, A), np.int32)
+    samples = []
+    for a in (1, 2):
+        ts = np.arange(T)
+        res = [okl.fit_slot(s.val[t, 0, a] - s.val[t, 0, 0], s.weight[t, 0, a], 4, 4, basis)
+               for t in ts]
+        wh = [r[0] for r in res]
+        wo = np.array([r[2] for r in res], np.float32)
+        od = np.array([r[3] for r in res])
+        coef[ts, 0, a] = wh
+        w_out[ts, 0, a] = wo
+        order_out[ts, 0, a] = od
+        samples.append(((ts, 0, a), (wh, wo, od)))
+    def gpu(c, w, o):
+        return [(c[ts, f, a], w[ts, f, a], o[ts, f, a]) for (ts, f, a), _ in samples]
+
+    ok = bench._oracle_sample_check(samples, gpu(coef, w_out, order_out), pp)
+    assert ok["ok"] and ok["slots"] == 2 * T and ok["coef_max_abs_err"] == 0.0
+    bad = order_out.copy()
+    bad[2, 0, 1] += 1
+    assert not bench._oracle_sample_check(samples, gpu(coef, w_out, bad), pp)["ok"]
+    badw = w_out.copy()
+    badw[3, 0, 2, 0] = 0.0 if badw[3, 0, 2, 0] > 0 else 1.0
+    assert not bench._oracle_sample_check(samples, gpu(coef, badw, order_out), pp)["ok"]
+    badc = coef.copy()
+    badc[1, 0, 2, 3] += 1e-3
+    r = bench._oracle_sample_check(samples, gpu(badc, w_out, order_out), pp)
+    assert not r["ok"] and r["slots_over_tol"] == 1 and r["over_tol_unexplained"] == 1
+
+
+def test_baseline_sample_is_the_cpu_baselines_sample():
+    """bench.baseline_sample (taken before the parity legs to snapshot the
+    GPU's outputs) picks the same slots cpu_baseline fits: deterministic,
+    never the reference station, one station and freq per worker."""
+    import numpy as np
+
+    import bench
+    from ska_sdp_screen_fitting_amd.synthetic import make_solutions
+
+    s = make_solutions(n_ant=5, n_time=9, n_freq=2, n_dir=4)
+    setup = {"ref_ant": 1}
+    a = bench.baseline_sample(s, setup, 6, slots_fit=4)
+    b = bench.baseline_sample(s, setup, 6, slots_fit=4)
+    assert len(a) == 6
+    for (ts, f, st), (ts2, f2, st2) in zip(a, b):
+        assert np.array_equal(ts, ts2) and f == f2 and st == st2
+        assert st != 1 and len(set(ts.tolist())) == 4 and f in (0, 1)

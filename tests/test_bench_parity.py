@@ -32,6 +32,31 @@ def test_parity_module_never_touches_the_oracle():
     assert not any(n.split(".")[0] == "oracle" for n in names), names
 
 
+def test_bench_imports_the_oracle_only_in_its_baseline_leg():
+    """bench.py may use the oracle only in the CPU baseline leg -- its
+    timed workers and the checker of the GPU fit on their sample -- never at
+    module level or in the measured GPU path."""
+    tree = ast.parse(open(os.path.join(REPO, "bench.py")).read())
+    allowed = {"_cpu_worker", "_oracle_sample_check"}
+    seen = set()
+
+    def visit(node, func):
+        for ch in ast.iter_child_nodes(node):
+            f = ch.name if isinstance(ch, (ast.FunctionDef, ast.AsyncFunctionDef)) else func
+            if isinstance(ch, ast.Import):
+                mods = [a.name for a in ch.names]
+            elif isinstance(ch, ast.ImportFrom):
+                mods = [ch.module or ""]
+            else:
+                mods = []
+            if any(m.split(".")[0] == "oracle" for m in mods):
+                seen.add(f)
+            visit(ch, f)
+
+    visit(tree, None)
+    assert seen and seen <= allowed, seen
+
+
 @pytest.mark.parametrize("name", sorted(set(bp.FIT_SETS.values())))
 def test_fit_sets_have_no_ill_conditioned_slot(name):
     """bench_parity compares every slot of its fit sets at 1e-8 with no

@@ -670,3 +670,53 @@ def test_binding_rejects_bad_device_operands(ctx, dev):
     ctx.eval(coef, S, out)  # the well-formed call still works
     torch.cuda.synchronize()
     assert torch.all(out[:, 0] == 1.0)
+
+
+@pytest.mark.parametrize("T", [6, 1000])
+def test_fit_vs_oracle_on_bench_workload_sample(ctx, dev, T):
+    """The fit exactly as bench.py runs it on config 4 (256 stations, 32
+    freqs, D = 20, setup_shard's reference phases and station orders; T
+    times) vs the oracle's fit_slot on 6 sampled times of 6 stations x 4
+    freqs: orders and flags equal, coefficients within 1e-8 x max(1,
+    |coef|max) -- the check the CPU baseline leg makes on its sample."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import WORKLOADS
+    from ska_sdp_screen_fitting_amd.distributed import setup_shard
+    from ska_sdp_screen_fitting_amd.synthetic import (FIELD_DEC_DEG, FIELD_RA_DEG,
+                                                      FIELD_WIDTH_DEG, make_solutions)
+    A, _, F, D, N, cell = WORKLOADS["config4"]
+    sol = make_solutions(n_ant=A, n_time=T, n_freq=F, n_dir=D, ant_offset=0, n_ant_total=A)
+    setup = setup_shard(sol, 0, A, FIELD_RA_DEG, FIELD_DEC_DEG, FIELD_WIDTH_DEG, cell,
+                        device="cpu")
+    ctx.set_basis(setup["piercepoints"], 100, 5.0 / 3.0)
+    phase = torch.from_numpy(sol.val).to(dev)
+    weight = torch.from_numpy(sol.weight).to(dev)
+    coef = torch.empty_like(phase)
+    resid = torch.empty_like(phase)
+    w_out = torch.empty_like(weight)
+    order_out = torch.empty((T, F, A), dtype=torch.int32, device=dev)
+    ctx.fit(phase, weight, T, F, A, setup["st_order"], niter=2, nsigma=5.0,
+            adjust_order=True, ref_ant=setup["ref_ant"], coef=coef, resid=resid,
+            w_out=w_out, order_out=order_out, ant_offset=setup["ant_offset"],
+            ref_phase=setup["ref_phase"].to(dev).contiguous())
+    torch.cuda.synchronize()
+    g_c, g_w, g_o = coef.cpu().numpy(), w_out.cpu().numpy(), order_out.cpu().numpy()
+    ref = setup["ref_ant"]
+    phi = sol.val - setup["ref_phase"].numpy()[:, :, None, :]
+    basis = okl.Basis(setup["piercepoints"])
+    scale = max(1.0, float(np.abs(g_c).max()))
+    bad = []
+    times = np.random.default_rng(3).choice(T, size=min(6, T), replace=False)
+    for a in [x for x in range(A) if x != ref][:6]:
+        so = setup["st_order"][a]
+        for f in range(4):
+            for t in times:
+                wh, _, wo, od, nf = okl.fit_slot(phi[t, f, a], sol.weight[t, f, a], so, so,
+                                                 basis)
+                dc = float(np.abs(g_c[t, f, a] - wh).max())
+                if g_o[t, f, a] != int(od) or not np.array_equal(g_w[t, f, a], wo) \
+                        or dc > 1e-8 * scale:
+                    bad.append((t, f, a, int(so), int(g_o[t, f, a]), int(od),
+                                int((g_w[t, f, a] > 0).sum()), int((wo > 0).sum()), nf, dc))
+    assert not bad, bad[:12]
