@@ -68,6 +68,14 @@ def parse():
                     help="skip the FITS-cube wall-clock legs (configs 1-3)")
     ap.add_argument("--no-fits-config3", action="store_true",
                     help="skip only the config-3 (107 GB, KL 256^2) FITS leg")
+    ap.add_argument("--cpu-fit-slots", type=int, default=64,
+                    help="CPU baseline: fit slots per worker (its oracle fits "
+                         "also check the GPU's fit of the same slots)")
+    ap.add_argument("--cpu-eval-slots", type=int, default=192,
+                    help="CPU baseline: evaluated slots per worker")
+    ap.add_argument("--no-cpu-reference-path", action="store_true",
+                    help="CPU baseline without the one-core make_aterm_image "
+                         "legs of configs 1 / 2")
     ap.add_argument("--cpu-workers", type=int, default=0,
                     help="CPU baseline pool size; 0 (default): this GPU's "
                          "share of the host (affinity / GPUs per node, capped "
@@ -336,11 +344,11 @@ def gpu_sample_outputs(torch, where, coef, w_out, order_out):
 def cpu_baseline(sol, setup, n_workers, rule="", slots_fit=64, slots_eval=192):
     import multiprocessing as mp
 
-    phi = sol.val - setup["ref_phase"].cpu().numpy()[:, :, None, :]
+    refph = setup["ref_phase"].cpu().numpy()
     jobs = []
     where = baseline_sample(sol, setup, n_workers, slots_fit)
     for ts, f, a in where:
-        jobs.append((phi[ts, f, a], sol.weight[ts, f, a],
+        jobs.append((sol.val[ts, f, a] - refph[ts, f], sol.weight[ts, f, a],
                      [setup["st_order"][a]] * len(ts), setup["piercepoints"],
                      (setup["x"], setup["y"]), slots_eval))
     ctx = mp.get_context("spawn")
@@ -917,15 +925,19 @@ def side_legs(ctx, torch, dev, stream, fit_stream, fit, evaluate, coef, bounds,
     return res
 
 
-def child_leg(extra, what, timeout_s=420, side=False):
+def child_leg(extra, what, timeout_s=420, side=False, oracle=False):
     """One workload of BASELINE.json beside the config-4 line, in a child
     ``bench.py`` (its own device buffers; the parent holds its own and is
     idle meanwhile): its value, eval roofline, checks and wall time; with
-    ``side``, also the child's eval alone on the chip (its side leg)."""
+    ``side``, also the child's eval alone on the chip (its side leg); with
+    ``oracle``, a small CPU baseline of its own (8 workers x 16 fit slots,
+    no make_aterm_image legs) whose oracle fits check the child's GPU fit."""
     import subprocess
+    base = (["--cpu-workers", "8", "--cpu-fit-slots", "16", "--cpu-eval-slots", "2",
+             "--no-cpu-reference-path"] if oracle else ["--no-cpu-baseline"])
     cmd = [sys.executable, os.path.abspath(__file__), "--gpus", "1",
-           "--no-cpu-baseline", "--no-fits", "--no-child-legs",
-           "--no-parity"] + ([] if side else ["--no-side-legs"]) + extra
+           "--no-fits", "--no-child-legs",
+           "--no-parity"] + base + ([] if side else ["--no-side-legs"]) + extra
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     t0 = time.perf_counter()
     try:
@@ -934,7 +946,8 @@ def child_leg(extra, what, timeout_s=420, side=False):
     except subprocess.TimeoutExpired:
         return {"error": f"timed out after {timeout_s} s", "args": extra}
     wall = time.perf_counter() - t0
-    if p.returncode != 0:
+    # exit 3: the child's line is printed, its parity (oracle sample) failed
+    if p.returncode not in (0, 3) or not p.stdout.strip():
         return {"error": f"exit {p.returncode}: {p.stderr[-600:]}", "args": extra}
     r = json.loads(p.stdout.strip().splitlines()[-1])
     rf, chk = r["roofline"], r["check"]
@@ -951,6 +964,9 @@ def child_leg(extra, what, timeout_s=420, side=False):
     if sm:
         out.update(sampled_slots=sm, checksums_match=sm.get("checksums_match"),
                    max_abs_err_vs_fp64=sm["max_abs_err_vs_fp64"], ok=sm["ok"])
+    if oracle and "oracle_check" in (r.get("cpu_baseline") or {}):
+        out["oracle_check"] = r["cpu_baseline"]["oracle_check"]
+        out["cpu_baseline_sample"] = r["cpu_baseline"]["sample"]
     alone = (r.get("side_legs") or {}).get("eval_fp32_sincos")
     if alone:
         # the same eval with nothing beside it (the step overlaps the fit of
@@ -978,7 +994,8 @@ def child_legs():
         "config5": child_leg(
             ["--workload", "config5", "--steps", "1", "--warmup", "1"],
             "one step of config 5's per-GPU shard in a child process "
-            "(bench.py --workload config5 --steps 1 --warmup 1)"),
+            "(bench.py --workload config5 --steps 1 --warmup 1), its fit "
+            "checked against the oracle on 128 sampled slots", oracle=True),
         "gain_config3": child_leg(
             ["--screen", "gain", "--workload", "config3", "--steps", "30", "--warmup", "2"],
             "gain screens on the config-3 shape in a child process", side=True),
@@ -1561,8 +1578,9 @@ def main():
         for c in range(n_chunks):
             fit(c, stream, 0)
         torch.cuda.synchronize(dev)
-        gpu_sample = gpu_sample_outputs(torch, baseline_sample(sol, setup, nw_cpu),
-                                        coef_sets[0], w_out, order_out)
+        gpu_sample = gpu_sample_outputs(
+            torch, baseline_sample(sol, setup, nw_cpu, args.cpu_fit_slots),
+            coef_sets[0], w_out, order_out)
     if (rank == 0 and world == 1 and args.workload == "config4" and not gain
             and not args.no_child_legs and not args.as_shard_of
             and not args.eval_only):
@@ -1692,7 +1710,8 @@ def main():
             nw, rule = cpu_share()
             if args.cpu_workers:
                 nw, rule = args.cpu_workers, "--cpu-workers"
-            line["cpu_baseline"] = cpu_baseline(sol, setup, max(1, nw), rule)
+            line["cpu_baseline"] = cpu_baseline(sol, setup, max(1, nw), rule,
+                                                args.cpu_fit_slots, args.cpu_eval_slots)
             samples = line["cpu_baseline"].pop("_samples")
             if gpu_sample is not None:
                 chk = _oracle_sample_check(samples, gpu_sample, setup["piercepoints"])
@@ -1705,13 +1724,23 @@ def main():
                 parity_failed = parity_failed or not chk["ok"]
             # BASELINE.json configs[0] / [1]: the CPU path of make_aterm_image
             # on one core, next to fits_wallclock.config1 / config2
-            legs = cpu_reference_path()
-            fw = line.get("fits_wallclock", {})
-            for k, v in legs.items():
-                if k in fw and "wall_s" in v:
-                    v["gpu_fits_wall_s"] = fw[k]["wall_s"]
-                    v["gpu_speedup"] = v["wall_s"] / fw[k]["wall_s"]
-            line["cpu_baseline"]["legs"] = legs
+            if not args.no_cpu_reference_path:
+                legs = cpu_reference_path()
+                fw = line.get("fits_wallclock", {})
+                for k, v in legs.items():
+                    if k in fw and "wall_s" in v:
+                        v["gpu_fits_wall_s"] = fw[k]["wall_s"]
+                        v["gpu_speedup"] = v["wall_s"] / fw[k]["wall_s"]
+                line["cpu_baseline"]["legs"] = legs
+        # the config-5 child leg's own oracle sample (its CPU baseline leg)
+        c5 = (side.get("config5") or {}).get("oracle_check")
+        if c5 is not None:
+            line.setdefault("parity", {})["fit_oracle_sample_config5"] = {
+                "max_err": c5["coef_max_abs_err"], "tol": c5["tol"], "ok": c5["ok"],
+                "slots": c5["slots"]}
+            if "all_ok" in line["parity"]:
+                line["parity"]["all_ok"] = line["parity"]["all_ok"] and c5["ok"]
+            parity_failed = parity_failed or not c5["ok"]
         line["library"] = dict(library_identity(), stale_counter_tables=dict(STALE_COUNTERS))
         print(json.dumps(line), flush=True)
     # release the CU-masked stream before the HIP runtime tears down
