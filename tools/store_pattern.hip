@@ -21,6 +21,7 @@
 //   tools/store_pattern [GiB [1]]   (1: the rhythm sweep -- s_sleep "compute"
 //   between store bursts, a barrier per group, LDS-capped occupancy)
 //   tools/store_pattern GiB 2 [R]   (2: long launches, R passes of the ring)
+//   tools/store_pattern GiB 3 [R]   (3: FMA "compute" vs sleep between bursts)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -123,9 +124,10 @@ __global__ __launch_bounds__(64 * NW) void contig(float* out, long P, long S, lo
 // the same two patterns with the eval's rhythm: `sl` s_sleep(1) ticks
 // (~64 clocks each) of "compute" before each group's stores, a workgroup
 // barrier per group (bar), and dynamic LDS to cap workgroups per CU
-template <int NW, int RUN>
+template <int NW, int RUN, bool VALU = false, int WAIT = 0>
 __global__ __launch_bounds__(64 * NW) void contig_t(float* out, long P, long S, long n_pb,
-                                                    long n_sc, int G, int xi, int sl, int bar) {
+                                                    long n_sc, int G, int xi, int sl, int bar,
+                                                    long ring = 0) {
   extern __shared__ float pad[];
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (sl < 0) pad[threadIdx.x] = 0.f;  // never: keeps the LDS allocation
@@ -133,11 +135,19 @@ __global__ __launch_bounds__(64 * NW) void contig_t(float* out, long P, long S, 
   item(blockIdx.x, n_pb, n_sc, 0, xi, pb, sc);
   if (sc >= n_sc) return;
   const long pix0 = pb * RUN;
-  const v4f v = {1.f, 2.f, 3.f, (float)l};
+  v4f v = {1.f, 2.f, 3.f, (float)l};
+  if (ring == 0) ring = S;
+  float x = (float)threadIdx.x;
   for (int g = 0; g < G; ++g) {
     const long s0 = (sc * G + g) * 16;
     if (s0 >= S) return;  // uniform per workgroup
-    for (int z = 0; z < sl; ++z) __builtin_amdgcn_s_sleep(1);
+    if (VALU) {
+      // sl dependent fp32 FMAs of "compute" (kept: folded into the value)
+      for (int z = 0; z < sl; ++z) x = __builtin_fmaf(x, 0.999f, 0.5f);
+      v[3] = x;
+    } else {
+      for (int z = 0; z < sl; ++z) __builtin_amdgcn_s_sleep(1);
+    }
     if (bar) __syncthreads();
     for (int j = 0; j < 16 / NW; ++j) {
       const long s = s0 + w * (16 / NW) + j;
@@ -147,9 +157,26 @@ __global__ __launch_bounds__(64 * NW) void contig_t(float* out, long P, long S, 
 #pragma unroll
         for (int c = 0; c < RUN / 256; ++c) {
           const long p = pix0 + c * 256 + 4 * l;
-          if (p < P) st(out + (s * 4 + q) * P + p, v);
+          if (p < P) st(out + ((s0 % ring + (s - s0)) * 4 + q) * P + p, v);
         }
     }
+    // WAIT 1: every wave waits for its stores of the group to complete
+    // before the next group (at most one burst in flight per wave)
+    if (WAIT == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (WAIT == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  }
+}
+
+// fill order with "compute": each wave writes `per` consecutive 1 KiB
+// float4 rows (a 16 KiB run at per = 16), `work` dependent FMAs before each
+__global__ __launch_bounds__(256) void lin_w(float* out, long n4, int per, int work) {
+  const long w = ((long)blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int l = threadIdx.x & 63;
+  float x = (float)l;
+  for (int k = 0; k < per; ++k) {
+    for (int z = 0; z < work; ++z) x = __builtin_fmaf(x, 0.999f, 0.5f);
+    const long i = (w * per + k) * 64 + l;
+    if (i < n4) st(out + 4 * i, v4f{1.f, 2.f, 3.f, x});
   }
 }
 
@@ -219,6 +246,64 @@ int main(int argc, char** argv) {
   });
   char name[128];
   const bool rhythm = argc > 2 && atoi(argv[2]) == 1;
+  if (argc > 2 && atoi(argv[2]) == 3) {
+    // round 5: does compute between store bursts (not sleep) speed the
+    // store stream?  fill order with FMAs between stores; the LDS16 order
+    // (256^2, 2 groups, interleaved map, one workgroup per CU by LDS, a
+    // barrier per group) with FMAs vs s_sleep between groups, long launches
+    const long n4 = bytes / 16;
+    for (int work : {0, 8, 32}) {
+      snprintf(name, sizeof name, "lin_w per16 work%-4d", work);
+      time(name, bytes, [&] {
+        hipLaunchKernelGGL(lin_w, dim3((unsigned)((n4 / 16 + 255) / 256 * 1)), dim3(256), 0, 0,
+                           out, n4, 16, work);
+      });
+    }
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&contig_t<16, 1024, true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 131584);
+    const long R = argc > 3 ? atol(argv[3]) : 16;
+    for (long N : {256L, 512L}) {
+      const long P = N * N;
+      const long ring = bytes / (16 * P);
+      const long S = ring * R;
+      const long wrote = S * 16 * P;
+      const int G = N == 256 ? 2 : 4;
+      const long n_sc = (S + 16 * G - 1) / (16 * G);
+      const long n_pb = P / 1024;
+      for (int work : {0, 64, 256}) {
+        snprintf(name, sizeof name, "lds16-like %ld^2 g%d fma%-5d bar1", N, G, work);
+        time(name, wrote, [&] {
+          hipLaunchKernelGGL((contig_t<16, 1024, true>), dim3((unsigned)(n_pb * n_sc)),
+                             dim3(1024), 131584, 0, out, P, S, n_pb, n_sc, G, 1, work, 1, ring);
+        });
+      }
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&contig_t<16, 1024, true, 1>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 131584);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&contig_t<16, 1024, true, 2>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 131584);
+      for (int work : {0, 64, 256}) {
+        snprintf(name, sizeof name, "lds16-like %ld^2 g%d fma%-5d bar1 wait0", N, G, work);
+        time(name, wrote, [&] {
+          hipLaunchKernelGGL((contig_t<16, 1024, true, 1>), dim3((unsigned)(n_pb * n_sc)),
+                             dim3(1024), 131584, 0, out, P, S, n_pb, n_sc, G, 1, work, 1, ring);
+        });
+        snprintf(name, sizeof name, "lds16-like %ld^2 g%d fma%-5d bar1 wait8", N, G, work);
+        time(name, wrote, [&] {
+          hipLaunchKernelGGL((contig_t<16, 1024, true, 2>), dim3((unsigned)(n_pb * n_sc)),
+                             dim3(1024), 131584, 0, out, P, S, n_pb, n_sc, G, 1, work, 1, ring);
+        });
+      }
+      for (int sl : {0, 16, 64}) {
+        snprintf(name, sizeof name, "lds16-like %ld^2 g%d sleep%-3d bar1", N, G, sl);
+        time(name, wrote, [&] {
+          hipLaunchKernelGGL((contig_t<16, 1024>), dim3((unsigned)(n_pb * n_sc)), dim3(1024),
+                             131584, 0, out, P, S, n_pb, n_sc, G, 1, sl, 1, ring);
+        });
+      }
+    }
+    (void)hipFree(out);
+    return 0;
+  }
   if (argc > 2 && atoi(argv[2]) == 2) {
     // long launches (round 5): the same orders over R passes of the ring in
     // ONE launch (slot s -> s mod ring, as the eval's ring), 40-80 ms per
