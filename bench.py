@@ -341,6 +341,25 @@ def gpu_sample_outputs(torch, where, coef, w_out, order_out):
     return out
 
 
+def amp_blocks(sol, n_blocks=4):
+    """Gain screens: the (freq, station, pol) amplitude blocks whose whole
+    time series the CPU baseline leg fits with the oracle (the outlier sigma
+    couples a block's times, Q6, so a block is the unit)."""
+    T, F, A, D = sol.val.shape
+    return [(k % F, (7 * k + 1) % A, k % 2) for k in range(n_blocks)]
+
+
+def gpu_amp_outputs(blocks, A, stacked, w_out, orders):
+    """The GPU amplitude fit's outputs of those blocks (pols stacked along
+    the station axis: pol p of station a is column p * A + a)."""
+    out = []
+    for f, a, p in blocks:
+        c = p * A + a
+        out.append((stacked[:, f, c].cpu().numpy(), w_out[:, f, c].cpu().numpy(),
+                    orders[:, f, c].cpu().numpy()))
+    return out
+
+
 def cpu_baseline(sol, setup, n_workers, rule="", slots_fit=64, slots_eval=192):
     import multiprocessing as mp
 
@@ -401,6 +420,37 @@ def cpu_baseline(sol, setup, n_workers, rule="", slots_fit=64, slots_eval=192):
         },
         "_samples": samples,
     }
+
+
+def _oracle_amp_check(blocks, gpu, sol, pp, order):
+    """Gain screens: the oracle's amplitude fit (oracle/kl.py
+    process_station_block: stationscreen.py:597-782 with the block sigma of
+    Q6, niter 3, as KLScreen.fit runs it, kl_screen.py:96-125) of whole
+    (freq, station, pol) blocks vs the GPU's stacked-pol fit of the same
+    blocks: orders and flags equal, coefficients <= 1e-8 x max(1, |coef|max)."""
+    sys.path.insert(0, REPO)
+    from oracle import kl as okl  # test infrastructure: the baseline leg's checker
+
+    basis = okl.Basis(pp)
+    n = n_ord = n_w = 0
+    err_max, scale = 0.0, 1.0
+    for g_c, _, _ in gpu:
+        scale = max(scale, float(np.nanmax(np.abs(g_c))))
+    for (f, a, p), (g_c, g_w, g_o) in zip(blocks, gpu):
+        v = sol.amp_val[:, f, a, :, p].T
+        w = sol.meta["amp_weight"][:, f, a, :, p].T
+        wh, _, wo, od = okl.process_station_block(v, w, order, basis, "amplitude", 3,
+                                                  5.0, True)
+        n += g_o.shape[0]
+        n_ord += int((g_o != od.astype(g_o.dtype)).sum())
+        n_w += int((g_w != wo.T).any(axis=-1).sum())
+        err_max = max(err_max, float(np.nanmax(np.abs(g_c - wh.T))))
+    ok = n_ord == 0 and n_w == 0 and err_max <= 1e-8 * scale
+    return {"blocks": len(blocks), "slots": n, "orders_differ": n_ord,
+            "weight_rows_differ": n_w, "coef_max_abs_err": err_max,
+            "coef_scale": scale, "tol": 1e-8 * scale, "ok": ok,
+            "what": "the GPU amplitude fit (stacked pols) vs the oracle's "
+                    "process_station_block on whole (freq, station, pol) blocks"}
 
 
 def _oracle_sample_check(samples, gpu, pp):
@@ -967,6 +1017,8 @@ def child_leg(extra, what, timeout_s=420, side=False, oracle=False):
     if oracle and "oracle_check" in (r.get("cpu_baseline") or {}):
         out["oracle_check"] = r["cpu_baseline"]["oracle_check"]
         out["cpu_baseline_sample"] = r["cpu_baseline"]["sample"]
+        if "oracle_amp_check" in r["cpu_baseline"]:
+            out["oracle_amp_check"] = r["cpu_baseline"]["oracle_amp_check"]
     alone = (r.get("side_legs") or {}).get("eval_fp32_sincos")
     if alone:
         # the same eval with nothing beside it (the step overlaps the fit of
@@ -998,7 +1050,10 @@ def child_legs():
             "checked against the oracle on 128 sampled slots", oracle=True),
         "gain_config3": child_leg(
             ["--screen", "gain", "--workload", "config3", "--steps", "30", "--warmup", "2"],
-            "gain screens on the config-3 shape in a child process", side=True),
+            "gain screens on the config-3 shape in a child process, its phase "
+            "fit checked against the oracle on 128 sampled slots and its "
+            "amplitude fit on 4 whole (freq, station, pol) blocks", side=True,
+            oracle=True),
         "tess_config3": child_leg(
             ["--screen", "tess", "--workload", "config3", "--steps", "10", "--warmup", "2"],
             "tessellated fill on the config-3 shape in a child process"),
@@ -1569,7 +1624,7 @@ def main():
     # the CPU baseline's sample of this workload's fit, taken now: the
     # parity and FITS legs below reuse this process's context with other
     # bases and grids
-    gpu_sample = None
+    gpu_sample = gpu_amp = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.eval_only:
         nw_cpu, rule_cpu = cpu_share()
         if args.cpu_workers:
@@ -1581,6 +1636,9 @@ def main():
         gpu_sample = gpu_sample_outputs(
             torch, baseline_sample(sol, setup, nw_cpu, args.cpu_fit_slots),
             coef_sets[0], w_out, order_out)
+        if gain:
+            gpu_amp = gpu_amp_outputs(amp_blocks(sol), A, amp_sets[0][0], amp["w_out"],
+                                      amp["orders"])
     if (rank == 0 and world == 1 and args.workload == "config4" and not gain
             and not args.no_child_legs and not args.as_shard_of
             and not args.eval_only):
@@ -1722,6 +1780,16 @@ def main():
                 if "all_ok" in line["parity"]:
                     line["parity"]["all_ok"] = line["parity"]["all_ok"] and chk["ok"]
                 parity_failed = parity_failed or not chk["ok"]
+            if gpu_amp is not None:
+                ach = _oracle_amp_check(amp_blocks(sol), gpu_amp, sol,
+                                        setup["piercepoints"], amp["order"])
+                line["cpu_baseline"]["oracle_amp_check"] = ach
+                line.setdefault("parity", {})["fit_oracle_amplitude_blocks"] = {
+                    "max_err": ach["coef_max_abs_err"], "tol": ach["tol"],
+                    "ok": ach["ok"], "slots": ach["slots"]}
+                if "all_ok" in line["parity"]:
+                    line["parity"]["all_ok"] = line["parity"]["all_ok"] and ach["ok"]
+                parity_failed = parity_failed or not ach["ok"]
             # BASELINE.json configs[0] / [1]: the CPU path of make_aterm_image
             # on one core, next to fits_wallclock.config1 / config2
             if not args.no_cpu_reference_path:
@@ -1732,10 +1800,16 @@ def main():
                         v["gpu_fits_wall_s"] = fw[k]["wall_s"]
                         v["gpu_speedup"] = v["wall_s"] / fw[k]["wall_s"]
                 line["cpu_baseline"]["legs"] = legs
-        # the config-5 child leg's own oracle sample (its CPU baseline leg)
-        c5 = (side.get("config5") or {}).get("oracle_check")
-        if c5 is not None:
-            line.setdefault("parity", {})["fit_oracle_sample_config5"] = {
+        # the child legs' own oracle samples (their CPU baseline legs)
+        for leg, key, pkey in (("config5", "oracle_check", "fit_oracle_sample_config5"),
+                               ("gain_config3", "oracle_check",
+                                "fit_oracle_sample_gain_config3"),
+                               ("gain_config3", "oracle_amp_check",
+                                "fit_oracle_amplitude_blocks_gain_config3")):
+            c5 = (side.get(leg) or {}).get(key)
+            if c5 is None:
+                continue
+            line.setdefault("parity", {})[pkey] = {
                 "max_err": c5["coef_max_abs_err"], "tol": c5["tol"], "ok": c5["ok"],
                 "slots": c5["slots"]}
             if "all_ok" in line["parity"]:

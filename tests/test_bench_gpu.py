@@ -69,14 +69,21 @@ def test_bench_line_carries_parity():
 
 
 @pytest.mark.gpu
-def test_cpu_baseline_leg_checks_the_fit_on_its_sample():
+@pytest.mark.parametrize("screen", ["phase", "gain"])
+def test_cpu_baseline_leg_checks_the_fit_on_its_sample(screen):
     """The CPU baseline leg's oracle fits (the sample it times) check the
     GPU's fit of the same slots of the benchmarked workload: orders and
     flags equal, coefficients within 1e-8 -- in the line as
-    cpu_baseline.oracle_check and parity.fit_oracle_sample."""
-    line = _bench("--cpu-baseline", "--cpu-workers", "4")
+    cpu_baseline.oracle_check and parity.fit_oracle_sample; for gain screens
+    also the amplitude fit of whole (freq, station, pol) blocks."""
+    extra = ["--screen", "gain"] if screen == "gain" else []
+    line = _bench("--cpu-baseline", "--cpu-workers", "4", "--no-cpu-reference-path", *extra)
     chk = line["cpu_baseline"]["oracle_check"]
     assert chk["ok"], chk
     assert chk["slots"] >= 16 and chk["orders_differ"] == 0
     assert line["parity"]["fit_oracle_sample"]["ok"]
     assert "_samples" not in line["cpu_baseline"]
+    if screen == "gain":
+        ach = line["cpu_baseline"]["oracle_amp_check"]
+        assert ach["ok"] and ach["blocks"] == 4, ach
+        assert line["parity"]["fit_oracle_amplitude_blocks"]["ok"]

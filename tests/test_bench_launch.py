@@ -264,3 +264,37 @@ def test_baseline_sample_is_the_cpu_baselines_sample():
     for (ts, f, st), (ts2, f2, st2) in zip(a, b):
         assert np.array_equal(ts, ts2) and f == f2 and st == st2
         assert st != 1 and len(set(ts.tolist())) == 4 and f in (0, 1)
+
+
+def test_oracle_amp_check_flags_mismatches():
+    """bench._oracle_amp_check (gain screens: the oracle's amplitude fit of
+    whole (freq, station, pol) blocks vs the GPU's): the oracle's own
+    outputs pass; a changed order or a coefficient off by 1e-6 fail."""
+    import numpy as np
+
+    import bench
+    from oracle import kl as okl
+    from ska_sdp_screen_fitting_amd import geometry
+    from ska_sdp_screen_fitting_amd.synthetic import make_amplitudes, make_solutions
+
+    T, F, A, D = 8, 2, 4, 6
+    s = make_solutions(n_ant=A, n_time=T, n_freq=F, n_dir=D)
+    make_amplitudes(s)
+    pp = geometry.piercepoints(s.dir_radec)[0]
+    basis = okl.Basis(pp)
+    order = 3
+    blocks = bench.amp_blocks(s, 3)
+    gpu = []
+    for f, a, p in blocks:
+        wh, _, wo, od = okl.process_station_block(
+            s.amp_val[:, f, a, :, p].T, s.meta["amp_weight"][:, f, a, :, p].T, order,
+            basis, "amplitude", 3, 5.0, True)
+        gpu.append((wh.T.copy(), wo.T.copy(), od.astype(np.int32)))
+    ok = bench._oracle_amp_check(blocks, gpu, s, pp, order)
+    assert ok["ok"] and ok["slots"] == 3 * T, ok
+    bad = [(c, w, o.copy()) for c, w, o in gpu]
+    bad[1][2][0] += 1
+    assert not bench._oracle_amp_check(blocks, bad, s, pp, order)["ok"]
+    badc = [(c.copy(), w, o) for c, w, o in gpu]
+    badc[2][0][3, 1] += 1e-6
+    assert not bench._oracle_amp_check(blocks, badc, s, pp, order)["ok"]
