@@ -501,6 +501,49 @@ def _oracle_sample_check(samples, gpu, pp):
                     "on the CPU baseline's sampled slots"}
 
 
+def tess_cpu_baseline(sol, setup, cell, lab, gpu_slot0, n_slots=64, slot=0):
+    """--screen tess, rank 0 at N = 1: the oracle's tessellated path
+    (oracle/voronoi.py: label_raster = voronoi_screen.py:218-351 restated
+    from the GEOS Polygonizer, gather_planes = voronoi_screen.py:177-214)
+    timed on one core for n_slots slots, and as the checker of the product:
+    its label raster vs the host template the GPU used, its gather of one
+    slot (``slot``: station ``slot`` at time 0, freq 0) vs the GPU's fill of
+    it (float32, <= 1 ulp)."""
+    sys.path.insert(0, REPO)
+    from oracle import voronoi as ov  # test infrastructure: the baseline leg
+    from ska_sdp_screen_fitting_amd.synthetic import (FIELD_DEC_DEG, FIELD_RA_DEG,
+                                                      FIELD_WIDTH_DEG)
+
+    rd = np.rad2deg(sol.dir_radec.astype(np.float64))
+    t0 = time.perf_counter()
+    lab_o, _ = ov.label_raster(rd[:, 0], rd[:, 1], FIELD_RA_DEG, FIELD_DEC_DEG,
+                               FIELD_WIDTH_DEG, cell)
+    t_lab = time.perf_counter() - t0
+    T, F, A, D = sol.val.shape
+    refph = setup["ref_phase"].cpu().numpy()
+    ph = (sol.val[0, 0] - refph[0, 0][None, :])[: max(min(n_slots, A), slot + 1)]
+    t0 = time.perf_counter()
+    planes = ov.gather_planes(lab_o, ph)
+    t_fill = time.perf_counter() - t0
+    n = ph.shape[0]
+    want = planes[slot]
+    ulp = int(np.abs(gpu_slot0.view(np.int32).astype(np.int64)
+                     - want.view(np.int32).astype(np.int64)).max())
+    labels_differ = int((lab_o != lab).sum())
+    ok = labels_differ == 0 and ulp <= 1
+    return {
+        "value": n / t_fill, "unit": "screen-slots/s", "cores": 1, "kind": "port",
+        "sample": (f"oracle gather_planes of {n} slots ({lab.shape[0]}^2, D = {D}) on "
+                   f"one core, {t_fill:.2f} s; its label raster {t_lab:.2f} s"),
+        "oracle_check": {"labels_differ": labels_differ, "max_ulp": ulp, "slots": 1,
+                         "max_err": float(ulp), "tol": 1.0, "ok": ok,
+                         "what": "the product's label template vs the oracle's "
+                                 "(GEOS-convention rings), and the GPU fill of "
+                                 f"slot {slot} (station {slot}, time 0, freq 0) "
+                                 "vs the oracle's gather"},
+    }
+
+
 def _affinity():
     try:
         return len(os.sched_getaffinity(0))
@@ -1016,7 +1059,7 @@ def child_leg(extra, what, timeout_s=420, side=False, oracle=False):
                    max_abs_err_vs_fp64=sm["max_abs_err_vs_fp64"], ok=sm["ok"])
     if oracle and "oracle_check" in (r.get("cpu_baseline") or {}):
         out["oracle_check"] = r["cpu_baseline"]["oracle_check"]
-        out["cpu_baseline_sample"] = r["cpu_baseline"]["sample"]
+        out["cpu_baseline_sample"] = r["cpu_baseline"].get("sample")
         if "oracle_amp_check" in r["cpu_baseline"]:
             out["oracle_amp_check"] = r["cpu_baseline"]["oracle_amp_check"]
     alone = (r.get("side_legs") or {}).get("eval_fp32_sincos")
@@ -1056,7 +1099,8 @@ def child_legs():
             oracle=True),
         "tess_config3": child_leg(
             ["--screen", "tess", "--workload", "config3", "--steps", "10", "--warmup", "2"],
-            "tessellated fill on the config-3 shape in a child process"),
+            "tessellated fill on the config-3 shape in a child process, its "
+            "label raster and slot-0 fill checked against the oracle", oracle=True),
     }
 
 
@@ -1186,9 +1230,12 @@ def tess_steps(args, ctx, torch, dev, dist, world, rank, coll_dev, sol, setup,
         cross = chk[:, 0] * chk[:, 3] - chk[:, 1] * chk[:, 2]
         mag = (chk[:, 0].hypot(chk[:, 1]) * chk[:, 2].hypot(chk[:, 3])).clamp(min=1e-30)
         unit_err, check_name = float((cross / mag).abs().max()), "max_rel_xx_yy_angle_cross"
+    # a slot of a station other than the reference (whose referenced phases
+    # are 0: every cell the same value, the labels untested)
+    k0 = 1 if setup["ref_ant"] == 0 and A > 1 else 0
     one = torch.empty((1, 4, N, N), dtype=torch.float32, device=dev)
-    ctx.tess_fill(lab_d, N, N, ph[:1], D, 1, one, smooth_pix=0.0, flags=flags)
-    p0 = ph[0].cpu().numpy()
+    ctx.tess_fill(lab_d, N, N, ph[k0:k0 + 1], D, 1, one, smooth_pix=0.0, flags=flags)
+    p0 = ph[k0].cpu().numpy()
     want = np.stack([np.cos(p0), np.sin(p0), np.cos(p0), np.sin(p0)]).astype(np.float32)
     want = want[:, lab - 1]
     got = one[0].cpu().numpy()
@@ -1237,7 +1284,20 @@ def tess_steps(args, ctx, torch, dev, dist, world, rank, coll_dev, sol, setup,
                       "slot0_max_ulp_vs_numpy_gather": ulp},
             "dist": dist_info,
         }
+        failed = False
+        if world == 1 and not args.no_cpu_baseline:
+            cb = tess_cpu_baseline(sol, setup, cell, lab, got, slot=k0)
+            line["cpu_baseline"] = cb
+            oc = cb["oracle_check"]
+            line["parity"] = {"tess_oracle_sample": {
+                "max_err": oc["max_err"], "tol": oc["tol"], "ok": oc["ok"],
+                "slots": oc["slots"], "labels_differ": oc["labels_differ"]},
+                "all_ok": oc["ok"]}
+            failed = not oc["ok"]
         print(json.dumps(line), flush=True)
+        if failed:
+            log("PARITY FAILED: the tessellated fill differs from the oracle")
+            raise SystemExit(3)
     if dist.is_initialized():
         dist.destroy_process_group()
 
@@ -1805,13 +1865,15 @@ def main():
                                ("gain_config3", "oracle_check",
                                 "fit_oracle_sample_gain_config3"),
                                ("gain_config3", "oracle_amp_check",
-                                "fit_oracle_amplitude_blocks_gain_config3")):
+                                "fit_oracle_amplitude_blocks_gain_config3"),
+                               ("tess_config3", "oracle_check",
+                                "tess_oracle_sample_config3")):
             c5 = (side.get(leg) or {}).get(key)
             if c5 is None:
                 continue
             line.setdefault("parity", {})[pkey] = {
-                "max_err": c5["coef_max_abs_err"], "tol": c5["tol"], "ok": c5["ok"],
-                "slots": c5["slots"]}
+                "max_err": c5.get("max_err", c5.get("coef_max_abs_err")),
+                "tol": c5["tol"], "ok": c5["ok"], "slots": c5["slots"]}
             if "all_ok" in line["parity"]:
                 line["parity"]["all_ok"] = line["parity"]["all_ok"] and c5["ok"]
             parity_failed = parity_failed or not c5["ok"]

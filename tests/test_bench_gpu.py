@@ -87,3 +87,14 @@ def test_cpu_baseline_leg_checks_the_fit_on_its_sample(screen):
         ach = line["cpu_baseline"]["oracle_amp_check"]
         assert ach["ok"] and ach["blocks"] == 4, ach
         assert line["parity"]["fit_oracle_amplitude_blocks"]["ok"]
+
+
+@pytest.mark.gpu
+def test_tess_cpu_baseline_leg_checks_labels_and_fill():
+    """--screen tess with its CPU baseline leg: the oracle's label raster
+    equals the product's template and the GPU's fill of a non-reference
+    slot equals the oracle's gather to 1 ulp -- parity.tess_oracle_sample."""
+    line = _bench("--cpu-baseline", "--screen", "tess")
+    oc = line["cpu_baseline"]["oracle_check"]
+    assert oc["ok"] and oc["labels_differ"] == 0 and oc["max_ulp"] <= 1, oc
+    assert line["parity"]["all_ok"] and line["parity"]["tess_oracle_sample"]["ok"]

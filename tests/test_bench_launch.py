@@ -298,3 +298,36 @@ def test_oracle_amp_check_flags_mismatches():
     badc = [(c.copy(), w, o) for c, w, o in gpu]
     badc[2][0][3, 1] += 1e-6
     assert not bench._oracle_amp_check(blocks, badc, s, pp, order)["ok"]
+
+
+def test_tess_cpu_baseline_checks_labels_and_fill():
+    """bench.tess_cpu_baseline (--screen tess): the oracle's label raster
+    and gather as the checker of the product's template and of the GPU's
+    slot-0 fill -- equal inputs pass, one changed label or a fill off by
+    more than 1 ulp fail."""
+    import numpy as np
+    import torch
+
+    import bench
+    from ska_sdp_screen_fitting_amd.synthetic import (FIELD_DEC_DEG, FIELD_RA_DEG,
+                                                      FIELD_WIDTH_DEG, make_solutions)
+    from ska_sdp_screen_fitting_amd.voronoi_screen import tessellation_template
+
+    cell = 0.2
+    s = make_solutions(n_ant=3, n_time=1, n_freq=1, n_dir=6)
+    setup = {"ref_phase": torch.from_numpy(np.ascontiguousarray(s.val[:, :, 0, :]))}
+    lab, _ = tessellation_template(np.rad2deg(s.dir_radec.astype(np.float64)),
+                                   FIELD_RA_DEG, FIELD_DEC_DEG, FIELD_WIDTH_DEG, cell)
+    p0 = s.val[0, 0, 1] - s.val[0, 0, 0]  # station 1, referenced to station 0
+    slot0 = np.stack([np.cos(p0), np.sin(p0), np.cos(p0), np.sin(p0)]).astype(np.float32)
+    slot0 = slot0[:, lab - 1]
+    r = bench.tess_cpu_baseline(s, setup, cell, lab, slot0, slot=1)
+    assert r["oracle_check"]["ok"], r
+    bad = lab.copy()
+    bad[3, 4] = bad[3, 4] % 6 + 1
+    assert not bench.tess_cpu_baseline(s, setup, cell, bad, slot0, slot=1)["oracle_check"]["ok"]
+    off = slot0.copy()
+    off[1, 2, 2] = np.nextafter(np.nextafter(off[1, 2, 2], 9.0, dtype=np.float32), 9.0,
+                                dtype=np.float32)
+    r = bench.tess_cpu_baseline(s, setup, cell, lab, off, slot=1)
+    assert r["oracle_check"]["max_ulp"] == 2 and not r["oracle_check"]["ok"]
