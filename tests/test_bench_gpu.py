@@ -68,6 +68,25 @@ def test_bench_line_carries_parity():
     assert line["library"]["sha16"]
 
 
+def _assert_contract(line, steps=3, warmup=1):
+    """The driver's bench-line contract: the keys, their types and the
+    roofline / cpu_baseline objects (BASELINE.json's metric)."""
+    base = json.load(open(os.path.join(REPO, "BASELINE.json")))
+    assert line["metric"] == base["metric"]
+    assert line["value"] > 0 and line["unit"] == "screen-slots/s"
+    assert line["n_gpus"] == 1 and line["steps"] == steps and line["warmup"] == warmup
+    assert line["ms_per_step"] > 0 and line["higher_is_better"] is True
+    assert line["scaling"] in ("weak", "strong") and line["vs_baseline"] is None
+    assert isinstance(line["dtype"], str) and line["data"] == "synthetic"
+    assert isinstance(line["config"]["workload"], str)
+    rf = line["roofline"]
+    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
+    assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-12 and "traffic" in rf
+    cb = line["cpu_baseline"]
+    assert cb["value"] > 0 and cb["unit"] == "screen-slots/s" and cb["cores"] >= 1
+    assert cb["kind"] in ("port", "reference") and cb["sample"]
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("screen", ["phase", "gain"])
 def test_cpu_baseline_leg_checks_the_fit_on_its_sample(screen):
@@ -83,6 +102,7 @@ def test_cpu_baseline_leg_checks_the_fit_on_its_sample(screen):
     assert chk["slots"] >= 16 and chk["orders_differ"] == 0
     assert line["parity"]["fit_oracle_sample"]["ok"]
     assert "_samples" not in line["cpu_baseline"]
+    _assert_contract(line)
     if screen == "gain":
         ach = line["cpu_baseline"]["oracle_amp_check"]
         assert ach["ok"] and ach["blocks"] == 4, ach
