@@ -195,12 +195,6 @@ int sf_device_cus(sf_ctx* ctx, int* n_cu);
  * bits (the rotations and their per-element arithmetic do not depend on how
  * a round's column pairs are split over the waves). */
 #define SF_OPT_FIT_EIG_WAVES 17
-/* SF_OPT_FIT_BATCH0 = 1: pass 0 of the phase fit for slots with every
- * direction unflagged and equal weights runs batched, 16 slots per wavefront
- * on f64 MFMA (the five mat-vecs of the eigenbasis solve); 0 = one slot per
- * wavefront group like every other slot.  Orders and flags are the same,
- * coefficients agree to the summation order (~1e-15 relative). */
-#define SF_OPT_FIT_BATCH0 18
 #define SF_EVAL_KERNEL_AUTO 0
 #define SF_EVAL_KERNEL_TILE 1
 #define SF_EVAL_KERNEL_LDS4 2

@@ -236,9 +236,6 @@ int sf_set_option(sf_ctx* ctx, int option, int value) {
                  "sf_set_option: eval workgroup waves must be 0, 4 or 8");
       ctx->eval_wg_waves = value;
       return SF_OK;
-    case SF_OPT_FIT_BATCH0:
-      ctx->fit_batch0 = value != 0;
-      return SF_OK;
     case SF_OPT_FIT_EIG_WAVES:
       SF_REQUIRE(value >= 0 && value <= 4, SF_EINVAL,
                  "sf_set_option: fit eig waves must be 0..4");

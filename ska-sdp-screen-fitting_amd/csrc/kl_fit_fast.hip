@@ -36,7 +36,6 @@ constexpr double kAtol = 1e-3;             // pinv(rcond=1e-3)
 constexpr size_t kLdsBytes = 160 * 1024;   // LDS of one gfx950 CU
 constexpr double kTinyW = 1e-3 * 1.001;    // slow-path threshold on weights
 constexpr unsigned long long kEmptyKey = 0ull;
-constexpr uint8_t kClassBatched = 3;       // pass 0 done by kl_fit_batch0_kernel
 
 __host__ __device__ inline int ldo(int n) { return n | 1; }
 
@@ -558,10 +557,6 @@ __global__ __launch_bounds__(256, SLOW ? 1 : SF_FIT_MINW) void kl_fit_pass_kerne
     // SLOW class tests its class first (it skips almost every slot).
     if (SLOW && cls[s] != want) continue;
     const uint8_t cl = SLOW ? want : cls[s];
-    // class 3: a full-mask uniform-weight slot whose pass-0 fit the batched
-    // kernel (kl_fit_batch0_kernel) already wrote to coef / resid; it is a
-    // class-0 slot in every other respect
-    const bool pre = !SLOW && cl == kClassBatched;
     const int a = (int)(s % A);
     const int p0 = pos[s];
     const int64_t base = s * D;
@@ -574,7 +569,7 @@ __global__ __launch_bounds__(256, SLOW ? 1 : SF_FIT_MINW) void kl_fit_pass_kerne
     }
     double order = (double)order_out[s];
     const double station_order = (double)st_order[a];
-    if (cl != want && !pre) continue;
+    if (cl != want) continue;
     int id = -1;
     if (p0 >= 0) {
       id = ids[p0];
@@ -640,9 +635,8 @@ __global__ __launch_bounds__(256, SLOW ? 1 : SF_FIT_MINW) void kl_fit_pass_kerne
     if (n_unfl > 0) {
       if (order > n_unfl - 1) order = n_unfl - 1;
       if (it == 0) {
-        if (!pre)
-          fit_once<SLOW, SPW, LEAN>(L, B, D, ld, (int)order, screen_type, uniform, wmin,
-                                    phi_p, w_p, phi_d, w_d, white_d, resid_d);
+        fit_once<SLOW, SPW, LEAN>(L, B, D, ld, (int)order, screen_type, uniform, wmin,
+                       phi_p, w_p, phi_d, w_d, white_d, resid_d);
       } else if (adjust_order) {
         bool hit_upper = false, hit_lower = false, hit_upper2 = false,
              hit_lower2 = false;
@@ -724,182 +718,6 @@ __global__ __launch_bounds__(256, SLOW ? 1 : SF_FIT_MINW) void kl_fit_pass_kerne
       w_out[base + d] = (float)w_d;
     }
     if (d == 0) order_out[s] = (int32_t)order;
-  }
-}
-
-// 4b. pass 0 of the PHASE fit for the full-mask uniform-weight slots,
-//     batched (round 5).  Those slots share the basis U and differ only in
-//     their order K, so fit_once's five mat-vecs become f64 MFMA tiles over
-//     16 slots per wavefront (v_mfma_f64_16x16x4f64: A = U or U^T fragments
-//     from LDS, B = the slots' vectors; a per-slot K is a column mask):
-//        a = U^T (w cos phi) / w,  U^T (w sin phi) / w   (rows < K, |lambda| > 1e-3)
-//        screen = atan2(U a_sin, U a_cos)
-//        s = U^T screen;  white = U (s / lambda),  C white = U s   (|lambda| > 1e-3)
-//        resid = phi - C white
-//     The 16x16x4 layouts chain without data movement: a lane (g = l / 16,
-//     j = l % 16) holds output rows 16 t + g + 4 r of slot j, and the next
-//     contraction's B operand at k-step kk = 4 t + r wants row 4 kk + g of
-//     slot j -- the same register.  Same arithmetic as fit_once up to the
-//     summation order of the MFMA dot products (and their fused
-//     multiply-adds): coefficients within ~1e-15 relative, orders and flags
-//     identical (tests/test_gpu_parity.py::test_fit_batch0_*).  The slots it
-//     takes become class 3; the pass kernel then only flags them.
-template <int TT>
-__global__ __launch_bounds__(256) void kl_fit_batch0_kernel(
-    int64_t S, int A, int D, const double* __restrict__ phase,
-    const double* __restrict__ refph, int ref_sub, const double* __restrict__ g_u,
-    const double* __restrict__ g_eig, const float* __restrict__ weight,
-    const int* __restrict__ pos, uint8_t* __restrict__ cls,
-    const int32_t* __restrict__ order0, double* __restrict__ coef,
-    double* __restrict__ resid) {
-#pragma clang fp contract(off)
-  typedef double v4d __attribute__((ext_vector_type(4)));
-  constexpr int KSM = 4 * TT;   // k-steps of a D <= 16 TT contraction
-  constexpr int NF = TT * KSM;  // fragments per matrix
-  extern __shared__ double frag[];  // [2][TT][KSM][64]: U^T, then U
-  using M = FitMath<true>;
-  const int ks = (D + 3) / 4;
-  for (int e = threadIdx.x; e < 2 * NF * 64; e += blockDim.x) {
-    const int ln = e & 63, f = (e >> 6) % NF, which = (e >> 6) / NF;
-    const int t = f / KSM, kk = f % KSM;
-    const int rr = 16 * t + (ln & 15), cc = 4 * kk + (ln >> 4);
-    double v = 0.0;
-    if (rr < D && cc < D) v = which == 0 ? g_u[cc * D + rr] : g_u[rr * D + cc];
-    frag[e] = v;
-  }
-  __syncthreads();
-  const double* FT = frag;            // FT[t][kk] lane l: U[4 kk + l/16][16 t + l%16]
-  const double* FU = frag + NF * 64;  // FU[t][kk] lane l: U[16 t + l%16][4 kk + l/16]
-  const int l = threadIdx.x & 63;
-  const int g = l >> 4, j = l & 15;
-  // per output row 16 t + g + 4 r: its eigenvalue and |lambda| > atol
-  double lam[KSM];
-  bool keep[KSM];
-#pragma unroll
-  for (int q = 0; q < KSM; ++q) {
-    const int row = 4 * q + g;  // = 16 t + g + 4 r for q = 4 t + r
-    lam[q] = row < D ? g_eig[row] : 0.0;
-    keep[q] = row < D && fabs(lam[q]) > kAtol;
-  }
-  const int64_t nb = (S + 15) / 16;
-  const int nwv = blockDim.x >> 6;
-  for (int64_t b = (int64_t)blockIdx.x * nwv + (threadIdx.x >> 6); b < nb;
-       b += (int64_t)gridDim.x * nwv) {
-    const int64_t s = b * 16 + j;
-    const bool in = s < S;
-    const int64_t sc = in ? s : S - 1;
-    const int a = (int)(sc % A);
-    const float w0 = weight[sc * D];
-    bool mism = false;
-    double phi[KSM];
-#pragma unroll
-    for (int q = 0; q < KSM; ++q) {
-      const int d = 4 * q + g;
-      phi[q] = 0.0;
-      if (q < ks && d < D) {
-        phi[q] = phase_ref(phase, refph, ref_sub, sc, a, A, D, d);
-        mism |= weight[sc * D + d] != w0;
-      }
-    }
-    // a slot takes this path when class 0, every direction unflagged and
-    // every weight equal (the four lanes of a column vote)
-    const unsigned long long bm = __ballot(mism);
-    const unsigned long long cm = (bm | (bm >> 16) | (bm >> 32) | (bm >> 48)) & 0xffffull;
-    const bool el = in && cls[sc] == 0 && pos[sc] == -1 && w0 > 0.0f && !((cm >> j) & 1ull);
-    if (__ballot(el) == 0ull) continue;  // wave-uniform
-    const double w = (double)w0;
-    int K = order0[sc];
-    if (K > D - 1) K = D - 1;
-    // ---- a = U^T v
-    v4d ac[TT], as[TT];
-#pragma unroll
-    for (int t = 0; t < TT; ++t) ac[t] = as[t] = v4d{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int q = 0; q < KSM; ++q) {
-      if (q >= ks) continue;  // uniform
-      const int d = 4 * q + g;
-      double sn = 0.0, cn = 0.0;
-      if (el && d < D) M::sin_cos(phi[q], &sn, &cn);
-      const double b0 = w * cn, b1 = w * sn;
-#pragma unroll
-      for (int t = 0; t < TT; ++t) {
-        const double f = FT[(t * KSM + q) * 64 + l];
-        ac[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(f, b0, ac[t], 0, 0, 0);
-        as[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(f, b1, as[t], 0, 0, 0);
-      }
-    }
-    // m(a): rows < K whose eigenvalue survives the cutoff (fit_once)
-    double m0[KSM], m1[KSM];
-#pragma unroll
-    for (int q = 0; q < KSM; ++q) {
-      const int row = 4 * q + g;
-      const bool k = keep[q] && row < K;
-      m0[q] = k ? ac[q >> 2][q & 3] / w : 0.0;
-      m1[q] = k ? as[q >> 2][q & 3] / w : 0.0;
-    }
-    // ---- C re = U m(a_cos), C im = U m(a_sin); screen = atan2
-    v4d cr[TT], ci[TT];
-#pragma unroll
-    for (int t = 0; t < TT; ++t) cr[t] = ci[t] = v4d{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int q = 0; q < KSM; ++q) {
-      if (q >= ks) continue;  // uniform
-#pragma unroll
-      for (int t = 0; t < TT; ++t) {
-        const double f = FU[(t * KSM + q) * 64 + l];
-        cr[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(f, m0[q], cr[t], 0, 0, 0);
-        ci[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(f, m1[q], ci[t], 0, 0, 0);
-      }
-    }
-    double scr[KSM];
-#pragma unroll
-    for (int q = 0; q < KSM; ++q) {
-      const int row = 4 * q + g;
-      scr[q] = (el && row < D) ? M::arctan2(ci[q >> 2][q & 3], cr[q >> 2][q & 3]) : 0.0;
-    }
-    // ---- s = U^T screen
-    v4d sh[TT];
-#pragma unroll
-    for (int t = 0; t < TT; ++t) sh[t] = v4d{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int q = 0; q < KSM; ++q) {
-      if (q >= ks) continue;  // uniform
-#pragma unroll
-      for (int t = 0; t < TT; ++t)
-        sh[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(FT[(t * KSM + q) * 64 + l], scr[q],
-                                                      sh[t], 0, 0, 0);
-    }
-#pragma unroll
-    for (int q = 0; q < KSM; ++q) {
-      const double v = sh[q >> 2][q & 3];
-      m0[q] = keep[q] ? v / lam[q] : 0.0;
-      m1[q] = keep[q] ? v : 0.0;
-    }
-    // ---- white = U (s / lambda), C white = U s
-    v4d wh[TT], cw[TT];
-#pragma unroll
-    for (int t = 0; t < TT; ++t) wh[t] = cw[t] = v4d{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int q = 0; q < KSM; ++q) {
-      if (q >= ks) continue;  // uniform
-#pragma unroll
-      for (int t = 0; t < TT; ++t) {
-        const double f = FU[(t * KSM + q) * 64 + l];
-        wh[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(f, m0[q], wh[t], 0, 0, 0);
-        cw[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(f, m1[q], cw[t], 0, 0, 0);
-      }
-    }
-    if (el) {
-#pragma unroll
-      for (int q = 0; q < KSM; ++q) {
-        const int d = 4 * q + g;
-        if (q < ks && d < D) {
-          coef[s * D + d] = wh[q >> 2][q & 3];
-          resid[s * D + d] = phi[q] - cw[q >> 2][q & 3];
-        }
-      }
-      if (g == 0) cls[s] = kClassBatched;
-    }
   }
 }
 
@@ -1158,33 +976,6 @@ static int launch_pass(sf_ctx* ctx, int it, const sf_fit_params* p,
                                          w_out, order_out);
 }
 
-// pass 0 of the phase fit for the full-mask uniform-weight slots, batched
-// (kl_fit_batch0_kernel): after kl_classify_kernel, before the passes
-static int launch_batch0(sf_ctx* ctx, const RefSpec& r, int64_t S, int A,
-                         const double* phase, const float* weight, double* coef,
-                         double* resid, int32_t* order_out) {
-  const int D = ctx->D;
-  const int64_t nb = (S + 15) / 16;
-  int64_t blocks = (nb + 3) / 4;
-  if (blocks > 4096) blocks = 4096;
-#define SF_LAUNCH_B0(TT)                                                              \
-  do {                                                                                \
-    const size_t shm = (size_t)2 * (TT) * 4 * (TT) * 64 * sizeof(double);              \
-    if (shm >= 64 * 1024)                                                             \
-      SF_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&kl_fit_batch0_kernel<TT>), \
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm)); \
-    hipLaunchKernelGGL(kl_fit_batch0_kernel<TT>, dim3((unsigned)blocks), dim3(256), shm, \
-                       ctx->stream, S, A, D, phase, r.refph, r.sub, ctx->d_u,          \
-                       ctx->d_eig, weight, ctx->d_pos, ctx->d_class, order_out, coef,  \
-                       resid);                                                        \
-  } while (0)
-  if (D <= 32) SF_LAUNCH_B0(2);
-  else SF_LAUNCH_B0(4);
-#undef SF_LAUNCH_B0
-  SF_HIP(hipGetLastError());
-  return SF_OK;
-}
-
 int launch_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,
                int F, int A, const sf_fit_params* p, double* coef,
                double* resid, float* w_out, int32_t* order_out) {
@@ -1280,8 +1071,6 @@ int launch_fit(sf_ctx* ctx, const double* phase, const float* weight, int T,
   }
 
   const bool block_flags = p->screen_type != SF_SCREEN_PHASE;
-  if (p->screen_type == SF_SCREEN_PHASE && ctx->fit_batch0 && D <= 64 && S > 0)
-    SF_TRYF(launch_batch0(ctx, r, S, A, phase, weight, coef, resid, order_out));
   for (int it = 0; it < p->niter; ++it) {
     int n_slow = 0, n_nonuniform = 0;
     SF_TRYF(number_and_decompose(ctx, &n_slow, &n_nonuniform));

@@ -128,7 +128,6 @@ struct sf_ctx {
   int tess_box = -1;            // SF_OPT_TESS_BOX (-1 auto, 0 wide-tile, 1 interior lookups)
   int fit_pack = 1;             // SF_OPT_FIT_PACK: 2 slots per wave for D <= 32
   int fit_lean = 1;             // SF_OPT_FIT_LEAN: lean pass when weights are uniform
-  int fit_batch0 = 0;           // SF_OPT_FIT_BATCH0: pass 0 of full-mask slots on MFMA
 };
 
 namespace sf {

@@ -720,76 +720,3 @@ def test_fit_vs_oracle_on_bench_workload_sample(ctx, dev, T):
                     bad.append((t, f, a, int(so), int(g_o[t, f, a]), int(od),
                                 int((g_w[t, f, a] > 0).sum()), int((wo > 0).sum()), nf, dc))
     assert not bad, bad[:12]
-
-
-def _fit_with(ctx, dev, g, batch0):
-    from ska_sdp_screen_fitting_amd._lib import SF_OPT_FIT_BATCH0
-    ctx.set_option(SF_OPT_FIT_BATCH0, batch0)
-    try:
-        return gpu_fit(ctx, dev, g)
-    finally:
-        ctx.set_option(SF_OPT_FIT_BATCH0, 0)
-
-
-@pytest.mark.parametrize("name", ["synth20", "synth50", "synth12tiny", "fixture_kl"])
-def test_fit_batch0_matches_per_slot_pass(ctx, dev, name):
-    """SF_OPT_FIT_BATCH0 (pass 0 of the full-mask uniform-weight slots
-    batched on f64 MFMA) vs the per-slot pass: orders and flagged weights
-    identical, coefficients and residuals to the summation order; and the
-    batched fit still matches the reference's own golden outputs."""
-    g = load_golden(name)
-    on = _fit_with(ctx, dev, g, 1)
-    off = _fit_with(ctx, dev, g, 0)
-    np.testing.assert_array_equal(on[3], off[3])
-    np.testing.assert_array_equal(on[2], off[2])
-    scale = max(1.0, np.abs(off[0]).max())
-    bad = _ill_conditioned(g)
-    keep = np.ones(off[0].shape[:3], bool)
-    for i in bad:
-        keep[i] = False
-    assert np.abs(on[0] - off[0])[keep].max() <= 1e-12 * scale
-    assert np.abs(on[1] - off[1])[keep].max() <= 1e-11
-    np.testing.assert_array_equal(on[3], g["orders"])
-    np.testing.assert_array_equal(on[2], g["w_out"])
-
-
-def test_fit_batch0_on_bench_workload(ctx, dev):
-    """The same on config 4's shape (256 stations x 32 freqs, D = 20, 12
-    times; ~80 % of the slots take the batched pass 0) and on the config-5
-    shard's (64 stations, D = 50, 512^2 basis, 4 times)."""
-    import sys
-    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    from bench import WORKLOADS
-    from ska_sdp_screen_fitting_amd._lib import SF_OPT_FIT_BATCH0
-    from ska_sdp_screen_fitting_amd.distributed import setup_shard
-    from ska_sdp_screen_fitting_amd.synthetic import (FIELD_DEC_DEG, FIELD_RA_DEG,
-                                                      FIELD_WIDTH_DEG, make_solutions)
-    for wl, A_, T in (("config4", None, 12), ("config5", 64, 4)):
-        A, _, F, D, N, cell = WORKLOADS[wl]
-        A = A_ or A
-        sol = make_solutions(n_ant=A, n_time=T, n_freq=F, n_dir=D, ant_offset=0,
-                             n_ant_total=A)
-        setup = setup_shard(sol, 0, A, FIELD_RA_DEG, FIELD_DEC_DEG, FIELD_WIDTH_DEG, cell,
-                            device="cpu")
-        ctx.set_basis(setup["piercepoints"], 100, 5.0 / 3.0)
-        phase = torch.from_numpy(sol.val).to(dev)
-        weight = torch.from_numpy(sol.weight).to(dev)
-        outs = []
-        for b in (1, 0):
-            coef = torch.empty_like(phase)
-            resid = torch.empty_like(phase)
-            w_out = torch.empty_like(weight)
-            order = torch.empty((T, F, A), dtype=torch.int32, device=dev)
-            ctx.set_option(SF_OPT_FIT_BATCH0, b)
-            ctx.fit(phase, weight, T, F, A, setup["st_order"], niter=2, nsigma=5.0,
-                    adjust_order=True, ref_ant=setup["ref_ant"], coef=coef, resid=resid,
-                    w_out=w_out, order_out=order, ant_offset=setup["ant_offset"],
-                    ref_phase=setup["ref_phase"].to(dev).contiguous())
-            torch.cuda.synchronize()
-            outs.append([x.cpu().numpy() for x in (coef, resid, w_out, order)])
-        ctx.set_option(SF_OPT_FIT_BATCH0, 0)
-        on, off = outs
-        np.testing.assert_array_equal(on[3], off[3], err_msg=wl)
-        np.testing.assert_array_equal(on[2], off[2], err_msg=wl)
-        scale = max(1.0, float(np.abs(off[0]).max()))
-        assert np.abs(on[0] - off[0]).max() <= 1e-11 * scale, wl
