@@ -320,7 +320,7 @@ def _cpu_worker(job):
 def baseline_sample(sol, setup, n_workers, slots_fit=64):
     """The CPU baseline's fit sample: per worker k, slots_fit random times
     of station k (skipping the reference station) at freq k mod F."""
-    T, F, A, D = sol.val.shape
+    T, F, A, _ = sol.val.shape
     ref = setup["ref_ant"]
     rng = np.random.default_rng(1)
     where = []
@@ -345,7 +345,7 @@ def amp_blocks(sol, n_blocks=4):
     """Gain screens: the (freq, station, pol) amplitude blocks whose whole
     time series the CPU baseline leg fits with the oracle (the outlier sigma
     couples a block's times, Q6, so a block is the unit)."""
-    T, F, A, D = sol.val.shape
+    _, F, A, _ = sol.val.shape
     return [(k % F, (7 * k + 1) % A, k % 2) for k in range(n_blocks)]
 
 
@@ -519,7 +519,7 @@ def tess_cpu_baseline(sol, setup, cell, lab, gpu_slot0, n_slots=64, slot=0):
     lab_o, _ = ov.label_raster(rd[:, 0], rd[:, 1], FIELD_RA_DEG, FIELD_DEC_DEG,
                                FIELD_WIDTH_DEG, cell)
     t_lab = time.perf_counter() - t0
-    T, F, A, D = sol.val.shape
+    A, D = sol.val.shape[2:]
     refph = setup["ref_phase"].cpu().numpy()
     ph = (sol.val[0, 0] - refph[0, 0][None, :])[: max(min(n_slots, A), slot + 1)]
     t0 = time.perf_counter()
@@ -1686,9 +1686,7 @@ def main():
     # bases and grids
     gpu_sample = gpu_amp = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.eval_only:
-        nw_cpu, rule_cpu = cpu_share()
-        if args.cpu_workers:
-            nw_cpu, rule_cpu = args.cpu_workers, "--cpu-workers"
+        nw_cpu = args.cpu_workers or cpu_share()[0]
         nw_cpu = max(1, nw_cpu)
         for c in range(n_chunks):
             fit(c, stream, 0)
