@@ -195,6 +195,12 @@ int sf_device_cus(sf_ctx* ctx, int* n_cu);
  * bits (the rotations and their per-element arithmetic do not depend on how
  * a round's column pairs are split over the waves). */
 #define SF_OPT_FIT_EIG_WAVES 17
+/* SF_OPT_FIT_SUBSET_DELETION = 1 (default): the flagged-direction subset
+ * bases from the global eigenbasis by one secular-equation deletion per
+ * flagged direction (Loewner-corrected vectors), the Jacobi solve only for
+ * the masks the deletions cannot separate; 0 = the Jacobi solve for every
+ * mask (D <= 64 either way). */
+#define SF_OPT_FIT_SUBSET_DELETION 18
 #define SF_EVAL_KERNEL_AUTO 0
 #define SF_EVAL_KERNEL_TILE 1
 #define SF_EVAL_KERNEL_LDS4 2

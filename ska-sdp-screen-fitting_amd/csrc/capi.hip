@@ -101,6 +101,7 @@ int sf_destroy(sf_ctx* ctx) {
   hipFree(ctx->d_ids);
   hipFree(ctx->d_pool_mask);
   hipFree(ctx->d_pool);
+  hipFree(ctx->d_pool_status);
   hipFree(ctx->d_pos);
   hipFree(ctx->d_sigma);
   hipFree(ctx->d_class);
@@ -235,6 +236,9 @@ int sf_set_option(sf_ctx* ctx, int option, int value) {
       SF_REQUIRE(value == 0 || value == 4 || value == 8, SF_EINVAL,
                  "sf_set_option: eval workgroup waves must be 0, 4 or 8");
       ctx->eval_wg_waves = value;
+      return SF_OK;
+    case SF_OPT_FIT_SUBSET_DELETION:
+      ctx->fit_subset_deletion = value != 0;
       return SF_OK;
     case SF_OPT_FIT_EIG_WAVES:
       SF_REQUIRE(value >= 0 && value <= 4, SF_EINVAL,

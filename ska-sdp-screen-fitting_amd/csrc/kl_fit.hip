@@ -94,8 +94,8 @@ __global__ __launch_bounds__(64) void kl_skip_kernel(
   const int f = blk / A, a = blk % A;
   const int d = lane();
   bool any_val = false, any_w = false;
-  if (d < D) {
-    for (int t = 0; t < T; ++t) {
+  for (int t = 0; t < T; ++t) {
+    if (d < D) {
       const int64_t base = ((int64_t)(t * F + f) * A) * D;
       double ph = phase[base + (int64_t)a * D + d];
       if (refph) ph -= refph[(int64_t)(t * F + f) * D + d];
@@ -103,6 +103,9 @@ __global__ __launch_bounds__(64) void kl_skip_kernel(
       any_val |= !isnan(ph);
       any_w |= weight[base + (int64_t)a * D + d] != 0.0f;
     }
+    // a block is kept as soon as it has one finite phase and one non-zero
+    // weight: stop there (every 8 times, a wave-uniform test)
+    if ((t & 7) == 7 && __any(any_val) && __any(any_w)) break;
   }
   const bool av = __any(any_val), aw = __any(any_w);
   if (d == 0) skip[blk] = (!av || !aw) ? 1 : 0;

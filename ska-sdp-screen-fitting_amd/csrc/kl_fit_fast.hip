@@ -97,8 +97,6 @@ __global__ __launch_bounds__(256) void kl_classify_kernel(
   float x = 0.0f;
   if (live) {
     x = weight[s * D + d];
-    coef[s * D + d] = 0.0;
-    resid[s * D + d] = 0.0;
     w_out[s * D + d] = x;
   }
   // the group's unflagged-direction bits and tiny-weight vote
@@ -113,9 +111,17 @@ __global__ __launch_bounds__(256) void kl_classify_kernel(
   const float w_first = __shfl(x, g * GW + (mask ? __builtin_ctzll(mask) : 0));
   const unsigned long long bn = __ballot(live && x > 0.0f && x != w_first);
   const bool nonuniform = ((bn >> (g * GW)) & gmask) != 0ull;
-  if (d != 0 || s >= S) return;
+  if (s >= S) return;
   const int a = (int)(s % A);
   const int f = (int)((s / A) % F);
+  // zero outputs only where no pass writes them: skipped blocks (class 1);
+  // the passes write every other slot (pass 0 starts from zero coefficients
+  // and residuals without reading them)
+  if (live && (a == ref_skip || skip[f * A + a])) {
+    coef[s * D + d] = 0.0;
+    resid[s * D + d] = 0.0;
+  }
+  if (d != 0) return;
   if (a == ref_skip || skip[f * A + a]) {  // stationscreen.py:818-825
     cls[s] = 1;
     order_out[s] = 0;
@@ -163,7 +169,8 @@ template <int NW>
 __global__ __launch_bounds__(64 * NW) void kl_subset_eig_kernel(
     const double* __restrict__ g_c, int D,
     const unsigned long long* __restrict__ pool_mask, int pool_cap,
-    int* __restrict__ counters, double* __restrict__ pool) {
+    int* __restrict__ counters, double* __restrict__ pool,
+    const uint8_t* __restrict__ done) {
   extern __shared__ double smem[];
   const int ld = subset_ld(D);
   double* a = smem;
@@ -177,6 +184,8 @@ __global__ __launch_bounds__(64 * NW) void kl_subset_eig_kernel(
   const int l = lane();
   const bool w0 = threadIdx.x < 64;  // NW waves per mask
   for (int id = first + blockIdx.x; id < last; id += gridDim.x) {
+    // masks the deletion kernel already decomposed (status 0)
+    if (done && done[id] == 0) continue;
     const unsigned long long m = pool_mask[id];
     const bool in = (l < D) && ((m >> l) & 1ull);
     const int n = __popcll(m);
@@ -205,6 +214,297 @@ __global__ __launch_bounds__(64 * NW) void kl_subset_eig_kernel(
       e[D * D + l] = a[pr * ld + pr];
     }
     __syncthreads();
+  }
+}
+
+// 3b. subset bases by deletions (round 5): the eigenpairs of the principal
+//     submatrix C_sub = C[idx][:, idx] follow from those of C = U diag(lam)
+//     U^T one deleted direction j at a time.  With z = row j of U, the
+//     eigenvalues mu of the matrix without row / column j are the roots of
+//         f(mu) = sum_i z_i^2 / (lam_i - mu) = 0
+//     (det(C_j - mu) / det(C - mu) = [(C - mu)^-1]_jj), one between each
+//     pair of consecutive poles, and its eigenvectors are U w with w_i ~
+//     z_i / (lam_i - mu) (row j of U w is f(mu) = 0).  Each root is found
+//     relative to its nearer pole (tau = mu - pole, Newton on tau rest(tau) -
+//     z_pole^2 inside a bisection bracket), and the z_i are recomputed from
+//     the roots by Loewner's formula before the vectors are formed
+//     (Gu & Eisenstat: the vectors then come out orthogonal to rounding).
+//     A direction whose z_i is negligible keeps its eigenpair (deflation).
+//     One wavefront per mask, k deletions for k flagged directions (in
+//     descending direction order, so the row of direction f is f), lane =
+//     root / row; O(k n^2) per lane against the Jacobi's ~8 sweeps of n - 1
+//     rounds.  Cases it does not take -- two poles closer than 1e-12 of the
+//     spectrum, a root that does not converge -- are left to the Jacobi
+//     kernel (status 1).  Eigenvalues to ~1e-15 of |lam|max and
+//     eigenvectors to the conditioning LAPACK's have (~1e-11 for
+//     close pairs), tests/test_gpu_parity.py::test_subset_secular_*.
+__global__ __launch_bounds__(64) void kl_subset_secular_kernel(
+    const double* __restrict__ g_u, const double* __restrict__ g_eig, int D,
+    const unsigned long long* __restrict__ pool_mask, int pool_cap,
+    int* __restrict__ counters, double* __restrict__ pool,
+    uint8_t* __restrict__ status) {
+#pragma clang fp contract(off)
+  extern __shared__ double smem[];
+  const int ld = D | 1;
+  double* U = smem;            // [D][ld] current eigenvectors (row = direction)
+  double* W = U + D * ld;      // [D][ld] w (row = non-deflated pole, col = root), then U w
+  double* lam = W + D * ld;    // [64] current eigenvalues, ascending
+  double* lz = lam + 64;       // [64] the non-deflated ones
+  double* zh = lz + 64;        // [64] their z (then Loewner's)
+  double* tau = zh + 64;       // [64] root - its pole
+  double* nlam = tau + 64;     // [64] next eigenvalues (unsorted)
+  int* ndi = reinterpret_cast<int*>(nlam + 64);  // [64] non-deflated pole -> column
+  int* orig = ndi + 64;        // [64] root -> its pole (index into lz)
+  int* src = orig + 64;        // [64] next slot -> root r, or -1 - deflated column
+  int* perm = src + 64;        // [64] an order
+  const int l = lane();
+  const int first = counters[1];
+  const int last = min(counters[0], pool_cap);
+  constexpr double kEps = 2.220446049250313e-16;
+  for (int id = first + blockIdx.x; id < last; id += gridDim.x) {
+    const unsigned long long msk = pool_mask[id];
+    const int n = __popcll(msk);
+    if (n >= D) {
+      if (l == 0) status[id] = 1;
+      continue;
+    }
+    // ---- the global basis in ascending eigenvalue order
+    const double li = l < D ? g_eig[l] : 0.0;
+    int rk = 0;
+    if (l < D)
+      for (int k = 0; k < D; ++k) {
+        const double lk = g_eig[k];
+        rk += (lk < li) || (lk == li && k < l);
+      }
+    if (l < D) perm[rk] = l;
+    lds_sync();
+    if (l < D) lam[l] = g_eig[perm[l]];
+    for (int e = l; e < D * D; e += 64) {
+      const int p = e / D, c = e % D;
+      U[p * ld + c] = g_u[p * D + perm[c]];
+    }
+    lds_sync();
+    int m = D;
+    bool ok = true;
+    for (int f = D - 1; f >= 0 && ok; --f) {
+      if ((msk >> f) & 1ull) continue;  // unflagged: stays
+      const int j = f;                  // its row (every deleted row so far is > f)
+      // ---- z, deflation of negligible components
+      const double z = l < m ? U[j * ld + l] : 0.0;
+      const double zmax = wave_max(fabs(z));
+      const double lmax = wave_max(l < m ? fabs(lam[l]) : 0.0);
+      const bool nd = l < m && fabs(z) > 1e-14 * zmax;
+      const unsigned long long ndm = __ballot(nd);
+      const int nn = __popcll(ndm);
+      const int kk = __builtin_amdgcn_mbcnt_hi((uint32_t)(ndm >> 32),
+                                               __builtin_amdgcn_mbcnt_lo((uint32_t)ndm, 0));
+      if (nd) {
+        ndi[kk] = l;
+        lz[kk] = lam[l];
+        zh[kk] = z;
+      }
+      lds_sync();
+      // two non-deflated poles too close to separate a root between them
+      const bool close = l + 1 < nn && lz[l + 1] - lz[l] <= 1e-12 * lmax;
+      if (__ballot(close) != 0ull) {
+        ok = false;
+        break;
+      }
+      // ---- roots: lane r < nn - 1 between poles r and r + 1, as
+      //      tau = mu - (nearer pole); Newton on tau rest(tau) - z_pole^2
+      //      (the nearer pole's term divided out) inside a bisection bracket
+      double t = 0.0;
+      int o = 0;
+      bool conv = true;
+      if (l + 1 < nn) {
+        const double lo = lz[l], hi = lz[l + 1];
+        const double mid = lo + 0.5 * (hi - lo);
+        double fm = 0.0;  // only its sign is used
+        for (int k = 0; k < nn; ++k) {
+          const double zk = zh[k];
+          const double x = lz[k] - mid;
+          double q = __builtin_amdgcn_rcp(x);
+          q = q * (2.0 - x * q);
+          fm += zk * zk * q;
+        }
+        double a, b;
+        if (fm >= 0.0) {
+          o = l;
+          a = 0.0;
+          b = mid - lo;
+        } else {
+          o = l + 1;
+          a = mid - hi;
+          b = 0.0;
+        }
+        const double lo_ = lz[o];
+        const double zo = zh[o];
+        const double zo2 = zo * zo;
+        t = 0.5 * (a + b);
+        conv = false;
+        for (int it = 0; it < 64; ++it) {
+          double rest = 0.0, drest = 0.0;
+          for (int k = 0; k < nn; ++k) {
+            const double zk = zh[k];
+            const double x = (lz[k] - lo_) - t;
+            // 1 / x: the hardware reciprocal and one Newton step (to ~1 ulp)
+            double q = __builtin_amdgcn_rcp(x);
+            q = q * (2.0 - x * q);
+            q = k == o ? 0.0 : q;
+            const double zq = zk * zk * q;
+            rest += zq;
+            drest += zq * q;
+          }
+          const double fv = rest - zo2 / t;  // increasing in t
+          if (fv == 0.0) {
+            conv = true;
+            break;
+          }
+          if (fv < 0.0) a = t; else b = t;
+          double tn = t - (t * rest - zo2) / (rest + t * drest);
+          if (fabs(tn - t) <= 4.0 * kEps * fabs(t)) {
+            t = tn;
+            conv = true;
+            break;
+          }
+          if (!(tn > a && tn < b)) tn = 0.5 * (a + b);
+          t = tn;
+          if (!(b - a > 4.0 * kEps * fmax(fabs(a), fabs(b)))) {
+            conv = true;
+            break;
+          }
+        }
+        tau[l] = t;
+        orig[l] = o;
+      }
+      if (__ballot(!conv) != 0ull) {
+        ok = false;
+        break;
+      }
+      lds_sync();
+      // ---- Loewner: z_k^2 = prod_r (mu_r - lam_k) / prod_{k' != k} (lam_k' - lam_k),
+      //      root r paired with pole r (r < k) or r + 1 (r >= k)
+      double zn = 0.0;
+      if (l < nn) {
+        const double lk = lz[l];
+        double pr = 1.0;
+        for (int r = 0; r + 1 < nn; ++r) {
+          const int kp = r < l ? r : r + 1;
+          pr *= ((lz[orig[r]] - lk) + tau[r]) / (lz[kp] - lk);
+        }
+        zn = sqrt(fabs(pr));
+        if (zh[l] < 0.0) zn = -zn;
+      }
+      lds_sync();
+      if (l < nn) zh[l] = zn;
+      lds_sync();
+      // ---- w columns (lane r = root), normalised
+      if (l + 1 < nn) {
+        const double ol = lz[o];
+        double nrm = 0.0;
+        for (int k = 0; k < nn; ++k) {
+          const double w = zh[k] / ((lz[k] - ol) - t);
+          W[k * ld + l] = w;
+          nrm += w * w;
+        }
+        const double inv = 1.0 / sqrt(nrm);
+        for (int k = 0; k < nn; ++k) W[k * ld + l] *= inv;
+      }
+      // next eigenvalues: the roots (slots 0 .. nn - 2), then the deflated
+      // poles (slots nn - 1 ..)
+      const int dk = l - kk;  // deflated lanes below this one
+      if (l + 1 < nn) {
+        nlam[l] = lz[o] + t;
+        src[l] = l;
+      }
+      if (l < m && !nd) {
+        nlam[nn - 1 + dk] = lam[l];
+        src[nn - 1 + dk] = -1 - l;
+      }
+      lds_sync();
+      // ---- U w into W's root columns (column r is read whole by every
+      //      lane before any lane writes it), deflated columns copied
+      if (l < m) {
+        // four root columns at a time: each U element read once per four
+        // products; no deflation (the common case) reads U's columns directly
+        const bool dense = nn == m;
+        int r = 0;
+        for (; r + 4 < nn; r += 4) {
+          double y0 = 0.0, y1 = 0.0, y2 = 0.0, y3 = 0.0;
+          for (int k = 0; k < nn; ++k) {
+            const double u = U[l * ld + (dense ? k : ndi[k])];
+            const double* wk = W + k * ld + r;
+            y0 += u * wk[0];
+            y1 += u * wk[1];
+            y2 += u * wk[2];
+            y3 += u * wk[3];
+          }
+          lds_sync();
+          W[l * ld + r] = y0;
+          W[l * ld + r + 1] = y1;
+          W[l * ld + r + 2] = y2;
+          W[l * ld + r + 3] = y3;
+        }
+        for (; r + 1 < nn; ++r) {
+          double y = 0.0;
+          for (int k = 0; k < nn; ++k) y += U[l * ld + (dense ? k : ndi[k])] * W[k * ld + r];
+          lds_sync();
+          W[l * ld + r] = y;
+        }
+        for (int c = 0; c < m - nn; ++c) {
+          const int sc = src[nn - 1 + c];
+          W[l * ld + nn - 1 + c] = U[l * ld + (-1 - sc)];
+        }
+      }
+      // ascending order of the m - 1 next eigenvalues
+      const int m1 = m - 1;
+      if (l < m1) {
+        const double v = nlam[l];
+        int r2 = 0;
+        for (int k = 0; k < m1; ++k) {
+          const double w = nlam[k];
+          r2 += (w < v) || (w == v && k < l);
+        }
+        perm[r2] = l;
+      }
+      lds_sync();
+      // ---- next U: rows without j, columns ascending
+      if (l < m && l != j) {
+        const int pn = l < j ? l : l - 1;
+        for (int c = 0; c < m1; ++c) U[pn * ld + c] = W[l * ld + perm[c]];
+      }
+      lds_sync();
+      if (l < m1) lam[l] = nlam[perm[l]];
+      for (int c = 0; c < m1; ++c) {
+        const double y = l < m1 ? U[l * ld + c] : 0.0;
+        const double nr = wave_sum(y * y);
+        if (l < m1) U[l * ld + c] = y / sqrt(nr);
+      }
+      lds_sync();
+      m = m1;
+    }
+    if (!ok) {
+      if (l == 0) status[id] = 1;
+      continue;
+    }
+    // ---- pool entry: columns by |mu| descending (wave_eig_order's rule)
+    if (l < m) {
+      const double v = fabs(lam[l]);
+      int r2 = 0;
+      for (int k = 0; k < m; ++k) {
+        const double w = fabs(lam[k]);
+        r2 += (w > v) || (w == v && k < l);
+      }
+      perm[r2] = l;
+    }
+    lds_sync();
+    double* e = pool + (size_t)id * (D * D + D);
+    if (l < m) {
+      for (int r = 0; r < m; ++r) e[l * D + r] = U[l * ld + perm[r]];
+      e[D * D + l] = lam[perm[l]];
+    }
+    if (l == 0) status[id] = 0;
+    lds_sync();
   }
 }
 
@@ -564,8 +864,9 @@ __global__ __launch_bounds__(256, SLOW ? 1 : SF_FIT_MINW) void kl_fit_pass_kerne
     if (d < D) {
       phi_d = phase_ref(phase, refph, ref_sub, s, a, A, D, d);
       w_d = (double)w_out[base + d];
-      white_d = coef[base + d];
-      resid_d = resid[base + d];
+      // pass 0 starts from zero (kl_classify_kernel leaves them unwritten)
+      white_d = it == 0 ? 0.0 : coef[base + d];
+      resid_d = it == 0 ? 0.0 : resid[base + d];
     }
     double order = (double)order_out[s];
     const double station_order = (double)st_order[a];
@@ -886,6 +1187,25 @@ static int number_and_decompose(sf_ctx* ctx, int* n_slow, int* n_nonuniform) {
     SF_HIP(hipGetLastError());
   }
   const int n_new = cnt[0] - cnt[1];
+  const uint8_t* done = nullptr;
+  if (n_new > 0 && ctx->fit_subset_deletion && ctx->D <= 64) {
+    // subset bases by deletions first (kl_subset_secular_kernel); the
+    // Jacobi below takes the masks it left (status 1)
+    SF_TRYF(grow(&ctx->d_pool_status, ctx->pool_status_cap, (size_t)cnt[0]));
+    const int D = ctx->D;
+    const int ldd = D | 1;
+    const size_t shm = (size_t)2 * D * ldd * sizeof(double) + 6 * 64 * sizeof(double) +
+                       4 * 64 * sizeof(int);
+    if (shm > 64 * 1024)
+      SF_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&kl_subset_secular_kernel),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+    const int blocks = n_new < 16384 ? n_new : 16384;
+    hipLaunchKernelGGL(kl_subset_secular_kernel, dim3(blocks), dim3(64), shm, ctx->stream,
+                       ctx->d_u, ctx->d_eig, D, ctx->d_pool_mask, (int)ctx->pool_cap,
+                       ctx->d_counters, ctx->d_pool, ctx->d_pool_status);
+    SF_HIP(hipGetLastError());
+    done = ctx->d_pool_status;
+  }
   if (n_new > 0) {
     const int D = ctx->D;
     const size_t shm = (size_t)2 * subset_rows(D) * subset_ld(D) * sizeof(double) +
@@ -900,7 +1220,7 @@ static int number_and_decompose(sf_ctx* ctx, int* n_slow, int* n_nonuniform) {
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm)); \
     hipLaunchKernelGGL(kl_subset_eig_kernel<NW>, dim3(blocks), dim3(64 * NW), shm,     \
                        ctx->stream, ctx->d_c, D, ctx->d_pool_mask, (int)ctx->pool_cap, \
-                       ctx->d_counters, ctx->d_pool);                                  \
+                       ctx->d_counters, ctx->d_pool, done);                            \
   } while (0)
     switch (nw) {
       case 1: SF_LAUNCH_EIG(1); break;

@@ -90,7 +90,10 @@ struct sf_ctx {
   unsigned long long* d_pool_mask = nullptr;  // [pool_cap] mask of pool entry
   double* d_pool = nullptr;              // [pool_cap][D*D + D] (U_sub, lam)
   int fit_eig_waves = 0;                 // SF_OPT_FIT_EIG_WAVES (0 = 3)
+  int fit_subset_deletion = 1;           // SF_OPT_FIT_SUBSET_DELETION (round 5: default)
   size_t pool_cap = 0;
+  uint8_t* d_pool_status = nullptr;      // [>= pool entries] deletion kernel: 0 done, 1 Jacobi
+  size_t pool_status_cap = 0;
   int pool_D = 0;
   int* d_pos = nullptr;                  // [S] table slot of the current mask
   uint8_t* d_class = nullptr;            // [S] 0 fast, 1 skipped, 2 slow

@@ -38,6 +38,7 @@ SF_OPT_TESS_BOX = 14
 SF_OPT_EVAL_INT = 15
 SF_OPT_EVAL_WG_WAVES = 16
 SF_OPT_FIT_EIG_WAVES = 17
+SF_OPT_FIT_SUBSET_DELETION = 18
 SF_EVAL_KERNEL_AUTO = 0
 SF_EVAL_KERNEL_TILE = 1
 SF_EVAL_KERNEL_LDS4 = 2

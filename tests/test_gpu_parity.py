@@ -132,9 +132,12 @@ def test_subset_jacobi_wave_count_is_bit_identical(ctx, dev, name):
     stationscreen.py:390-430 / :495-499 per flagged mask) on 1, 2, 3 (the
     default) and 4 waves per mask: the same pool of subset bases, bit for
     bit, and the same orders, flags, coefficients and residuals."""
-    from ska_sdp_screen_fitting_amd._lib import SF_OPT_FIT_EIG_WAVES
+    from ska_sdp_screen_fitting_amd._lib import (SF_OPT_FIT_EIG_WAVES,
+                                                 SF_OPT_FIT_SUBSET_DELETION)
     g = _wave_count_case(name)
     runs = {}
+    # the Jacobi solve for every mask (the deletions are the default)
+    ctx.set_option(SF_OPT_FIT_SUBSET_DELETION, 0)
     try:
         for nw in (3, 1, 2, 4):
             ctx.set_option(SF_OPT_FIT_EIG_WAVES, nw)
@@ -142,6 +145,7 @@ def test_subset_jacobi_wave_count_is_bit_identical(ctx, dev, name):
             runs[nw] = (out, ctx.fit_pool())
     finally:
         ctx.set_option(SF_OPT_FIT_EIG_WAVES, 0)
+        ctx.set_option(SF_OPT_FIT_SUBSET_DELETION, 1)
     (ref_out, (ref_masks, ref_pool)) = runs[3]
     assert len(ref_masks) > (100 if name == "config5-density" else 0)
     assert len(np.unique(ref_masks)) == len(ref_masks)
@@ -720,3 +724,52 @@ def test_fit_vs_oracle_on_bench_workload_sample(ctx, dev, T):
                     bad.append((t, f, a, int(so), int(g_o[t, f, a]), int(od),
                                 int((g_w[t, f, a] > 0).sum()), int((wo > 0).sum()), nf, dc))
     assert not bad, bad[:12]
+
+
+@pytest.mark.parametrize("name", ["synth50", "config5-density", "synth20", "fixture_kl"])
+def test_subset_deletion_bases_match_jacobi(ctx, dev, name):
+    """SF_OPT_FIT_SUBSET_DELETION: the subset bases by secular-equation
+    deletions from the global eigenbasis vs the Jacobi solve of each mask --
+    the same masks, eigenvalues to 1e-12 of |lambda|max, each eigenvector
+    to the conditioning of its eigenvalue gap (sign free), and the fit's
+    orders and flags identical, coefficients within 1e-9 of the golden."""
+    from ska_sdp_screen_fitting_amd._lib import SF_OPT_FIT_SUBSET_DELETION
+    g = _wave_count_case(name) if name == "config5-density" else load_golden(name)
+    ctx.set_option(SF_OPT_FIT_SUBSET_DELETION, 0)
+    try:
+        jac = gpu_fit(ctx, dev, g)
+        masks_j, pool_j = ctx.fit_pool()
+    finally:
+        ctx.set_option(SF_OPT_FIT_SUBSET_DELETION, 1)
+    dele = gpu_fit(ctx, dev, g)
+    masks_d, pool_d = ctx.fit_pool()
+    assert np.array_equal(masks_j, masks_d)
+    D = g["val"].shape[-1]
+    lmax = 0.0
+    worst_l = worst_v = 0.0
+    for m, ej, ed in zip(masks_j, pool_j, pool_d):
+        n = bin(int(m)).count("1")
+        lj, ld_ = ej[D * D:D * D + n], ed[D * D:D * D + n]
+        lmax = max(lmax, np.abs(lj).max())
+        worst_l = max(worst_l, np.abs(lj - ld_).max())
+        Vj = ej[:D * D].reshape(D, D)[:n, :n]
+        Vd = ed[:D * D].reshape(D, D)[:n, :n]
+        sg = np.sign(np.sum(Vj * Vd, axis=0))
+        gap = np.full(n, np.inf)
+        srt = np.sort(lj)
+        for r in range(n):
+            d = np.abs(srt - lj[r])
+            d = d[d > 0]
+            gap[r] = d.min() if d.size else np.inf
+        err = np.abs(Vd * sg - Vj).max(axis=0)
+        worst_v = max(worst_v, float(np.max(err * gap / lmax)))
+    assert worst_l <= 1e-12 * lmax, (worst_l, lmax)
+    assert worst_v <= 1e-12, worst_v
+    np.testing.assert_array_equal(dele[3], jac[3])
+    np.testing.assert_array_equal(dele[2], jac[2])
+    scale = max(1.0, np.abs(jac[0]).max())
+    keep = np.ones(jac[0].shape[:3], bool)
+    if name != "config5-density":
+        for i in _ill_conditioned(g):
+            keep[i] = False
+    assert np.abs(dele[0] - jac[0])[keep].max() <= 1e-9 * scale

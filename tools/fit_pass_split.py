@@ -1,6 +1,7 @@
 """Where the fit pass's time goes: the batched KL fit (sf_kl_fit, phase,
 adjust_order) of a bench workload with niter 1 (pass 0 without the outlier
-flagging) and niter 2 (the bench's), each timed with HIP events over 3 calls;
+flagging) and niter 2 (the bench's), each timed with HIP events over 3 calls,
+then the bench's fit with SF_OPT_FIT_SUBSET_DELETION off / on (alternating);
 run under rocprofv3 --kernel-trace --stats for the per-kernel split.
 
     python tools/fit_pass_split.py [workload] [times]
@@ -16,6 +17,7 @@ sys.path.insert(0, os.path.join(REPO, "ska-sdp-screen-fitting_amd"))
 sys.path.insert(0, REPO)
 from bench import WORKLOADS  # noqa: E402
 from ska_sdp_screen_fitting_amd import get_context  # noqa: E402
+from ska_sdp_screen_fitting_amd._lib import SF_OPT_FIT_SUBSET_DELETION  # noqa: E402
 from ska_sdp_screen_fitting_amd.distributed import setup_shard  # noqa: E402
 from ska_sdp_screen_fitting_amd.synthetic import (FIELD_DEC_DEG, FIELD_RA_DEG,  # noqa: E402
                                                   FIELD_WIDTH_DEG, make_solutions)
@@ -40,7 +42,9 @@ coef = torch.empty_like(phase)
 resid = torch.empty_like(phase)
 w_out = torch.empty_like(weight)
 order_out = torch.empty((T, F, A), dtype=torch.int32, device=dev)
-for niter, adjust in ((1, True), (2, False), (2, True)):
+runs = [(1, True, 0), (2, False, 0), (2, True, 0)] + [(2, True, v) for v in (0, 1, 0, 1)]
+for niter, adjust, dele in runs:
+    ctx.set_option(SF_OPT_FIT_SUBSET_DELETION, dele)
     def run():
         ctx.fit(phase, weight, T, F, A, setup["st_order"], niter=niter, nsigma=5.0,
                 adjust_order=adjust, ref_ant=setup["ref_ant"], coef=coef, resid=resid,
@@ -57,5 +61,5 @@ for niter, adjust in ((1, True), (2, False), (2, True)):
         e1.record(stream)
         e1.synchronize()
         ms.append(e0.elapsed_time(e1))
-    print(f"{wl} S={T * F * A} niter={niter} adjust_order={adjust}: "
+    print(f"{wl} S={T * F * A} niter={niter} adjust_order={adjust} deletion={dele}: "
           f"{np.median(ms):.2f} ms  {ctx.fit_stats()}", flush=True)
