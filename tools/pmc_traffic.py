@@ -129,7 +129,8 @@ def fit_entry(d, workload, label, trace=None):
     command when given (``avg_ms``), else the slower durations under
     collection (``avg_ms_under_pmc``)."""
     kernels = {}
-    for k in ("kl_fit_pass_kernel", "kl_subset_eig_kernel", "kl_classify_kernel",
+    for k in ("kl_fit_pass_kernel", "kl_subset_secular_kernel", "kl_subset_eig_kernel",
+              "kl_classify_kernel",
               "kl_assign_kernel", "kl_fit_general_kernel"):
         try:
             r = summary(d, k, trace)
