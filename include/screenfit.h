@@ -196,10 +196,12 @@ int sf_device_cus(sf_ctx* ctx, int* n_cu);
  * a round's column pairs are split over the waves). */
 #define SF_OPT_FIT_EIG_WAVES 17
 /* SF_OPT_FIT_SUBSET_DELETION = 1 (default): the flagged-direction subset
- * bases from the global eigenbasis by one secular-equation deletion per
- * flagged direction (Loewner-corrected vectors), the Jacobi solve only for
- * the masks the deletions cannot separate; 0 = the Jacobi solve for every
- * mask (D <= 64 either way). */
+ * bases by secular-equation deletions (Loewner-corrected vectors), one per
+ * flagged direction, each mask starting from its nearest already
+ * decomposed ancestor in the mask table (the mask with its lowest flagged
+ * directions unflagged; the global basis when none is), the Jacobi solve
+ * only for the masks the deletions cannot separate; 2 = the same deletions,
+ * every mask from the global basis; 0 = the Jacobi solve for every mask. */
 #define SF_OPT_FIT_SUBSET_DELETION 18
 #define SF_EVAL_KERNEL_AUTO 0
 #define SF_EVAL_KERNEL_TILE 1

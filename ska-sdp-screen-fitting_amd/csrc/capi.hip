@@ -238,7 +238,9 @@ int sf_set_option(sf_ctx* ctx, int option, int value) {
       ctx->eval_wg_waves = value;
       return SF_OK;
     case SF_OPT_FIT_SUBSET_DELETION:
-      ctx->fit_subset_deletion = value != 0;
+      SF_REQUIRE(value >= 0 && value <= 2, SF_EINVAL,
+                 "SF_OPT_FIT_SUBSET_DELETION must be 0, 1 or 2");
+      ctx->fit_subset_deletion = (int)value;
       return SF_OK;
     case SF_OPT_FIT_EIG_WAVES:
       SF_REQUIRE(value >= 0 && value <= 4, SF_EINVAL,

@@ -62,6 +62,20 @@ __device__ int table_insert(unsigned long long* keys, int cap,
   return -3;
 }
 
+// The slot of `key` in the table, or -1 (read-only: the table does not
+// change while the subset bases are decomposed).
+__device__ int table_find(const unsigned long long* keys, int cap,
+                          unsigned long long key) {
+  int h = (int)(mix64(key) & (unsigned long long)(cap - 1));
+  for (int probe = 0; probe < cap; ++probe) {
+    const unsigned long long k = keys[h];
+    if (k == key) return h;
+    if (k == kEmptyKey) return -1;
+    h = (h + 1) & (cap - 1);
+  }
+  return -1;
+}
+
 __device__ __forceinline__ double phase_ref(const double* phase,
                                             const double* refph, int sub,
                                             int64_t s, int a, int A, int D,
@@ -142,7 +156,7 @@ __global__ __launch_bounds__(256) void kl_classify_kernel(
 __global__ __launch_bounds__(256) void kl_assign_kernel(
     const unsigned long long* __restrict__ keys, int cap, int* __restrict__ ids,
     unsigned long long* __restrict__ pool_mask, int pool_cap,
-    int* __restrict__ counters) {
+    int* __restrict__ counters, int D) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= cap) return;
   const unsigned long long k = keys[i];
@@ -150,6 +164,8 @@ __global__ __launch_bounds__(256) void kl_assign_kernel(
     const int id = atomicAdd(counters, 1);
     ids[i] = id;
     if (id < pool_cap) pool_mask[id] = k;
+    // the most flagged directions among the new masks (the deletion levels)
+    atomicMax(counters + 5, D - __popcll(k));
   }
 }
 
@@ -238,11 +254,21 @@ __global__ __launch_bounds__(64 * NW) void kl_subset_eig_kernel(
 //     kernel (status 1).  Eigenvalues to ~1e-15 of |lam|max and
 //     eigenvectors to the conditioning LAPACK's have (~1e-11 for
 //     close pairs), tests/test_gpu_parity.py::test_subset_secular_*.
+//
+//     Ancestors (level > 0): the launch takes the masks with `level` flagged
+//     directions, launches run level 1, 2, ... in order, and a mask starts
+//     from its nearest decomposed ancestor -- the mask with its lowest
+//     flagged directions unflagged, whose deletions are the first ones of
+//     its own (found in the mask table; decomposed by an earlier call, or by
+//     this call's lower levels without falling back) -- so a mask whose
+//     parent is in the pool costs one deletion instead of one per flagged
+//     direction.  level 0: every new mask from the global basis.
 __global__ __launch_bounds__(64) void kl_subset_secular_kernel(
     const double* __restrict__ g_u, const double* __restrict__ g_eig, int D,
     const unsigned long long* __restrict__ pool_mask, int pool_cap,
     int* __restrict__ counters, double* __restrict__ pool,
-    uint8_t* __restrict__ status) {
+    uint8_t* __restrict__ status, const unsigned long long* __restrict__ keys,
+    const int* __restrict__ ids, int table_cap, int level) {
 #pragma clang fp contract(off)
   extern __shared__ double smem[];
   const int ld = D | 1;
@@ -264,30 +290,73 @@ __global__ __launch_bounds__(64) void kl_subset_secular_kernel(
   for (int id = first + blockIdx.x; id < last; id += gridDim.x) {
     const unsigned long long msk = pool_mask[id];
     const int n = __popcll(msk);
+    if (level > 0 && D - n != level) continue;  // another launch's
     if (n >= D) {
       if (l == 0) status[id] = 1;
       continue;
     }
-    // ---- the global basis in ascending eigenvalue order
-    const double li = l < D ? g_eig[l] : 0.0;
-    int rk = 0;
-    if (l < D)
-      for (int k = 0; k < D; ++k) {
-        const double lk = g_eig[k];
-        rk += (lk < li) || (lk == li && k < l);
+    // ---- the nearest decomposed ancestor (wave-uniform search)
+    const unsigned long long full = D == 64 ? ~0ull : (1ull << D) - 1ull;
+    unsigned long long anc = full;
+    int aid = -1;
+    if (level > 0) {
+      unsigned long long a = msk;
+      for (;;) {
+        const unsigned long long fl = full & ~a;
+        a |= fl & (~fl + 1ull);  // unflag the lowest flagged direction
+        if (a == full) break;
+        const int h = table_find(keys, table_cap, a);
+        const int pid = h >= 0 ? ids[h] : -1;
+        if (pid >= 0 && pid < pool_cap && (pid < first || status[pid] == 0)) {
+          anc = a;
+          aid = pid;
+          break;
+        }
       }
-    if (l < D) perm[rk] = l;
-    lds_sync();
-    if (l < D) lam[l] = g_eig[perm[l]];
-    for (int e = l; e < D * D; e += 64) {
-      const int p = e / D, c = e % D;
-      U[p * ld + c] = g_u[p * D + perm[c]];
+    }
+    int m;
+    if (aid < 0) {
+      // ---- the global basis in ascending eigenvalue order
+      const double li = l < D ? g_eig[l] : 0.0;
+      int rk = 0;
+      if (l < D)
+        for (int k = 0; k < D; ++k) {
+          const double lk = g_eig[k];
+          rk += (lk < li) || (lk == li && k < l);
+        }
+      if (l < D) perm[rk] = l;
+      lds_sync();
+      if (l < D) lam[l] = g_eig[perm[l]];
+      for (int e = l; e < D * D; e += 64) {
+        const int p = e / D, c = e % D;
+        U[p * ld + c] = g_u[p * D + perm[c]];
+      }
+      m = D;
+    } else {
+      // ---- the ancestor's pool entry (rows = its directions ascending,
+      //      columns by |mu| descending) in ascending eigenvalue order
+      m = __popcll(anc);
+      const double* ea = pool + (size_t)aid * (D * D + D);
+      const double li = l < m ? ea[D * D + l] : 0.0;
+      int rk = 0;
+      if (l < m)
+        for (int k = 0; k < m; ++k) {
+          const double lk = ea[D * D + k];
+          rk += (lk < li) || (lk == li && k < l);
+        }
+      if (l < m) perm[rk] = l;
+      lds_sync();
+      if (l < m) lam[l] = ea[D * D + perm[l]];
+      for (int e = l; e < m * m; e += 64) {
+        const int p = e / m, c = e % m;
+        U[p * ld + c] = ea[p * D + perm[c]];
+      }
     }
     lds_sync();
-    int m = D;
     bool ok = true;
     for (int f = D - 1; f >= 0 && ok; --f) {
       if ((msk >> f) & 1ull) continue;  // unflagged: stays
+      if (!((anc >> f) & 1ull)) continue;  // deleted in the ancestor
       const int j = f;                  // its row (every deleted row so far is > f)
       // ---- z, deflation of negligible components
       const double z = l < m ? U[j * ld + l] : 0.0;
@@ -320,6 +389,7 @@ __global__ __launch_bounds__(64) void kl_subset_secular_kernel(
         const double lo = lz[l], hi = lz[l + 1];
         const double mid = lo + 0.5 * (hi - lo);
         double fm = 0.0;  // only its sign is used
+#pragma unroll 4
         for (int k = 0; k < nn; ++k) {
           const double zk = zh[k];
           const double x = lz[k] - mid;
@@ -344,6 +414,7 @@ __global__ __launch_bounds__(64) void kl_subset_secular_kernel(
         conv = false;
         for (int it = 0; it < 64; ++it) {
           double rest = 0.0, drest = 0.0;
+#pragma unroll 4
           for (int k = 0; k < nn; ++k) {
             const double zk = zh[k];
             const double x = (lz[k] - lo_) - t;
@@ -388,6 +459,7 @@ __global__ __launch_bounds__(64) void kl_subset_secular_kernel(
       if (l < nn) {
         const double lk = lz[l];
         double pr = 1.0;
+#pragma unroll 4
         for (int r = 0; r + 1 < nn; ++r) {
           const int kp = r < l ? r : r + 1;
           pr *= ((lz[orig[r]] - lk) + tau[r]) / (lz[kp] - lk);
@@ -402,6 +474,7 @@ __global__ __launch_bounds__(64) void kl_subset_secular_kernel(
       if (l + 1 < nn) {
         const double ol = lz[o];
         double nrm = 0.0;
+#pragma unroll 4
         for (int k = 0; k < nn; ++k) {
           const double w = zh[k] / ((lz[k] - ol) - t);
           W[k * ld + l] = w;
@@ -431,6 +504,7 @@ __global__ __launch_bounds__(64) void kl_subset_secular_kernel(
         int r = 0;
         for (; r + 4 < nn; r += 4) {
           double y0 = 0.0, y1 = 0.0, y2 = 0.0, y3 = 0.0;
+#pragma unroll 2
           for (int k = 0; k < nn; ++k) {
             const double u = U[l * ld + (dense ? k : ndi[k])];
             const double* wk = W + k * ld + r;
@@ -461,6 +535,7 @@ __global__ __launch_bounds__(64) void kl_subset_secular_kernel(
       if (l < m1) {
         const double v = nlam[l];
         int r2 = 0;
+#pragma unroll 4
         for (int k = 0; k < m1; ++k) {
           const double w = nlam[k];
           r2 += (w < v) || (w == v && k < l);
@@ -475,11 +550,20 @@ __global__ __launch_bounds__(64) void kl_subset_secular_kernel(
       }
       lds_sync();
       if (l < m1) lam[l] = nlam[perm[l]];
-      for (int c = 0; c < m1; ++c) {
-        const double y = l < m1 ? U[l * ld + c] : 0.0;
-        const double nr = wave_sum(y * y);
-        if (l < m1) U[l * ld + c] = y / sqrt(nr);
+      // column norms without row j (lane = column, rows summed in order;
+      // ~1 to rounding: row j of U w is f(mu) = 0), then each row rescaled
+      if (l < m1) {
+        double nr = 0.0;
+#pragma unroll 4
+        for (int r = 0; r < m1; ++r) {
+          const double y = U[r * ld + l];
+          nr += y * y;
+        }
+        tau[l] = sqrt(nr);
       }
+      lds_sync();
+      if (l < m1)
+        for (int c = 0; c < m1; ++c) U[l * ld + c] = U[l * ld + c] / tau[c];
       lds_sync();
       m = m1;
     }
@@ -1167,14 +1251,15 @@ __global__ __launch_bounds__(256) void kl_fill_mask_kernel(
 static int number_and_decompose(sf_ctx* ctx, int* n_slow, int* n_nonuniform) {
   SF_HIP(hipMemcpyAsync(ctx->d_counters + 1, ctx->d_counters, sizeof(int),
                         hipMemcpyDeviceToDevice, ctx->stream));
+  SF_HIP(hipMemsetAsync(ctx->d_counters + 5, 0, sizeof(int), ctx->stream));
   const int cap = (int)ctx->table_cap;
   const int old_cap = (int)ctx->pool_cap;
   hipLaunchKernelGGL(kl_assign_kernel, dim3((cap + 255) / 256), dim3(256), 0,
                      ctx->stream, ctx->d_keys, cap, ctx->d_ids,
-                     ctx->d_pool_mask, old_cap, ctx->d_counters);
+                     ctx->d_pool_mask, old_cap, ctx->d_counters, ctx->D);
   SF_HIP(hipGetLastError());
-  int cnt[5];
-  SF_HIP(hipMemcpyAsync(cnt, ctx->d_counters, 5 * sizeof(int),
+  int cnt[6];
+  SF_HIP(hipMemcpyAsync(cnt, ctx->d_counters, 6 * sizeof(int),
                         hipMemcpyDeviceToHost, ctx->stream));
   SF_HIP(hipStreamSynchronize(ctx->stream));
   *n_slow = cnt[2];
@@ -1200,10 +1285,17 @@ static int number_and_decompose(sf_ctx* ctx, int* n_slow, int* n_nonuniform) {
       SF_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&kl_subset_secular_kernel),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
     const int blocks = n_new < 16384 ? n_new : 16384;
-    hipLaunchKernelGGL(kl_subset_secular_kernel, dim3(blocks), dim3(64), shm, ctx->stream,
-                       ctx->d_u, ctx->d_eig, D, ctx->d_pool_mask, (int)ctx->pool_cap,
-                       ctx->d_counters, ctx->d_pool, ctx->d_pool_status);
-    SF_HIP(hipGetLastError());
+    // option 1: levels 1 .. (most flagged directions), each mask from its
+    // nearest decomposed ancestor; 2: one launch, every mask from the
+    // global basis
+    const int levels = ctx->fit_subset_deletion == 2 ? 0 : cnt[5];
+    for (int lv = levels > 0 ? 1 : 0; lv <= levels; ++lv) {
+      hipLaunchKernelGGL(kl_subset_secular_kernel, dim3(blocks), dim3(64), shm, ctx->stream,
+                         ctx->d_u, ctx->d_eig, D, ctx->d_pool_mask, (int)ctx->pool_cap,
+                         ctx->d_counters, ctx->d_pool, ctx->d_pool_status, ctx->d_keys,
+                         ctx->d_ids, cap, lv);
+      SF_HIP(hipGetLastError());
+    }
     done = ctx->d_pool_status;
   }
   if (n_new > 0) {

@@ -90,7 +90,7 @@ struct sf_ctx {
   unsigned long long* d_pool_mask = nullptr;  // [pool_cap] mask of pool entry
   double* d_pool = nullptr;              // [pool_cap][D*D + D] (U_sub, lam)
   int fit_eig_waves = 0;                 // SF_OPT_FIT_EIG_WAVES (0 = 3)
-  int fit_subset_deletion = 1;           // SF_OPT_FIT_SUBSET_DELETION (round 5: default)
+  int fit_subset_deletion = 1;           // SF_OPT_FIT_SUBSET_DELETION: 1 from ancestors (default), 2 from the global basis, 0 Jacobi
   size_t pool_cap = 0;
   uint8_t* d_pool_status = nullptr;      // [>= pool entries] deletion kernel: 0 done, 1 Jacobi
   size_t pool_status_cap = 0;

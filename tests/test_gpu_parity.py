@@ -726,23 +726,27 @@ def test_fit_vs_oracle_on_bench_workload_sample(ctx, dev, T):
     assert not bad, bad[:12]
 
 
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("name", ["synth50", "config5-density", "synth20", "fixture_kl"])
-def test_subset_deletion_bases_match_jacobi(ctx, dev, name):
+def test_subset_deletion_bases_match_jacobi(ctx, dev, name, mode):
     """SF_OPT_FIT_SUBSET_DELETION: the subset bases by secular-equation
     deletions from the global eigenbasis vs the Jacobi solve of each mask --
     the same masks, eigenvalues to 1e-12 of |lambda|max, each eigenvector
     to the conditioning of its eigenvalue gap (sign free), and the fit's
-    orders and flags identical, coefficients within 1e-9 of the golden."""
+    orders and flags identical, coefficients within 1e-9 of the golden.
+    mode 1 (the default): each mask from its nearest decomposed ancestor;
+    mode 2: every mask from the global basis."""
     from ska_sdp_screen_fitting_amd._lib import SF_OPT_FIT_SUBSET_DELETION
     g = _wave_count_case(name) if name == "config5-density" else load_golden(name)
     ctx.set_option(SF_OPT_FIT_SUBSET_DELETION, 0)
     try:
         jac = gpu_fit(ctx, dev, g)
         masks_j, pool_j = ctx.fit_pool()
+        ctx.set_option(SF_OPT_FIT_SUBSET_DELETION, mode)
+        dele = gpu_fit(ctx, dev, g)
+        masks_d, pool_d = ctx.fit_pool()
     finally:
         ctx.set_option(SF_OPT_FIT_SUBSET_DELETION, 1)
-    dele = gpu_fit(ctx, dev, g)
-    masks_d, pool_d = ctx.fit_pool()
     assert np.array_equal(masks_j, masks_d)
     D = g["val"].shape[-1]
     lmax = 0.0
@@ -772,4 +776,103 @@ def test_subset_deletion_bases_match_jacobi(ctx, dev, name):
     if name != "config5-density":
         for i in _ill_conditioned(g):
             keep[i] = False
+    assert np.abs(dele[0] - jac[0])[keep].max() <= 1e-9 * scale
+
+
+def _deletion_edge_case(name):
+    """Flag masks at the deletion kernel's edges: many deletions per mask
+    (D = 50, 25 % of the entries zero), the largest D (SF_MAX_DIR = 60),
+    a tiny D (masks down to one direction), and directions on a
+    square lattice, whose C has six exactly degenerate eigenvalue pairs (the
+    close-pole case the kernel hands to the Jacobi)."""
+    from ska_sdp_screen_fitting_amd import geometry
+    from ska_sdp_screen_fitting_amd.synthetic import make_solutions
+    n_dir, flag = {"heavy50": (50, 0.25), "d60": (60, 0.05), "d4": (4, 0.4),
+                   "lattice25": (25, 0.05)}[name]
+    s = make_solutions(n_ant=8, n_time=30, n_freq=2, n_dir=n_dir, seed=71,
+                       flag_frac=flag, outlier_frac=0.005)
+    pp, _, _ = geometry.piercepoints(s.dir_radec)
+    if name == "lattice25":
+        g = np.arange(5) - 2.0
+        X, Y = np.meshgrid(g, g)
+        pp = np.zeros((25, 3))
+        pp[:, 0], pp[:, 1] = X.ravel() * 900.0, Y.ravel() * 900.0
+    return dict(val=s.val, weight=s.weight, ant_pos=s.ant_pos, piercepoints=pp,
+                ref_ant=okl.reference_station(s.weight), order=min(20, n_dir))
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("name", ["heavy50", "d60", "d4", "lattice25"])
+def test_subset_deletion_edge_cases(ctx, dev, name, mode):
+    """The deletion subset bases vs the Jacobi's at the kernel's edges
+    (`_deletion_edge_case`): eigenvalues to 1e-12 of |lambda|max and
+    eigenvectors to their gap's conditioning everywhere; orders, flags and
+    coefficients as the Jacobi's where no eigenvalue is degenerate; on the
+    lattice, the masks whose first deletion meets the degenerate pairs come
+    back from the Jacobi fallback bit for bit."""
+    from ska_sdp_screen_fitting_amd._lib import SF_OPT_FIT_SUBSET_DELETION
+    g = _deletion_edge_case(name)
+    ctx.set_option(SF_OPT_FIT_SUBSET_DELETION, 0)
+    try:
+        jac = gpu_fit(ctx, dev, g)
+        masks_j, pool_j = ctx.fit_pool()
+        ctx.set_option(SF_OPT_FIT_SUBSET_DELETION, mode)
+        dele = gpu_fit(ctx, dev, g)
+        masks_d, pool_d = ctx.fit_pool()
+    finally:
+        ctx.set_option(SF_OPT_FIT_SUBSET_DELETION, 1)
+    assert len(masks_j) > (5 if name == "d4" else 20)
+    assert np.array_equal(masks_j, masks_d)
+    D = g["val"].shape[-1]
+    ns = [bin(int(m)).count("1") for m in masks_j]
+    if name == "heavy50":
+        assert np.mean([D - n for n in ns]) > 8  # many deletions per mask
+    if name == "d4":
+        assert min(ns) == 1
+    lmax = max(np.abs(e[D * D:D * D + n]).max() for e, n in zip(pool_j, ns))
+    c = ctx.get_basis()[0]
+    worst_l = worst_v = 0.0
+    same = 0
+    for m, n, ej, ed in zip(masks_j, ns, pool_j, pool_d):
+        lj, ld_ = ej[D * D:D * D + n], ed[D * D:D * D + n]
+        # both against LAPACK on the principal submatrix of the library's C
+        keep = [d for d in range(D) if (int(m) >> d) & 1]
+        lref = np.sort(np.linalg.eigvalsh(c[np.ix_(keep, keep)]))
+        assert np.abs(np.sort(lj) - lref).max() <= 1e-12 * lmax, ("jacobi", hex(int(m)), lj, lref)
+        assert np.abs(np.sort(ld_) - lref).max() <= 1e-12 * lmax, ("deletion", hex(int(m)), ld_, lref)
+        same += np.array_equal(ej[:D * D + n].view(np.uint64), ed[:D * D + n].view(np.uint64))
+        # columns paired by eigenvalue: two eigenvalues of equal |lambda| and
+        # opposite sign (a 2 x 2 subset of a zero-diagonal C: +-b) may come in
+        # either order from either solver, as from the reference's SVD
+        oj, od = np.argsort(lj, kind="stable"), np.argsort(ld_, kind="stable")
+        lj, ld_ = lj[oj], ld_[od]
+        worst_l = max(worst_l, np.abs(lj - ld_).max())
+        Vj = ej[:D * D].reshape(D, D)[:n, :n][:, oj]
+        Vd = ed[:D * D].reshape(D, D)[:n, :n][:, od]
+        sg = np.sign(np.sum(Vj * Vd, axis=0))
+        gap = np.array([np.min(np.abs(np.delete(lj, r) - lj[r]), initial=np.inf)
+                        for r in range(n)])
+        gap[~np.isfinite(gap)] = 0.0
+        err = np.abs(Vd * sg - Vj).max(axis=0)
+        worst_v = max(worst_v, float(np.max(err * gap / lmax)))
+    assert worst_l <= 1e-12 * lmax, (worst_l, lmax)
+    assert worst_v <= 1e-12, worst_v
+    if name == "lattice25":
+        assert same > 0  # the fallback ran
+        return
+    np.testing.assert_array_equal(dele[3], jac[3])
+    np.testing.assert_array_equal(dele[2], jac[2])
+    # coefficients, except where the slot's subset basis has two eigenvalues
+    # of equal |lambda| (order between them undefined, the order-K truncation
+    # may keep either; the case above, only at D = 4 here)
+    tie = set()
+    for m, n, ej in zip(masks_j, ns, pool_j):
+        a = np.sort(np.abs(ej[D * D:D * D + n]))
+        if n > 1 and np.min(np.diff(a)) <= 1e-9 * lmax:
+            tie.add(int(m))
+    bits = (dele[2] > 0).astype(np.uint64) << np.arange(D, dtype=np.uint64)
+    slot_mask = bits.sum(axis=-1)
+    keep = ~np.isin(slot_mask, np.array(sorted(tie), dtype=np.uint64))
+    assert name == "d4" or not tie
+    scale = max(1.0, np.abs(jac[0]).max())
     assert np.abs(dele[0] - jac[0])[keep].max() <= 1e-9 * scale

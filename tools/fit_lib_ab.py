@@ -106,6 +106,7 @@ def main():
             "weights_equal": bool(np.array_equal(wa, wb)),
             "weights_differ": int((wa != wb).sum()),
             "coef_max_rel": float(np.nanmax(np.abs(ca - cb)) / scale),
+            "coef_bit_equal": bool(np.array_equal(ca.view(np.uint64), cb.view(np.uint64))),
         }
         for li in range(2):
             for k in ("order", "w", "coef"):
