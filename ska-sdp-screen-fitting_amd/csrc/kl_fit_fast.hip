@@ -24,6 +24,7 @@
 // passes the new masks are inserted, numbered and decomposed.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 
@@ -55,7 +56,10 @@ __device__ int table_insert(unsigned long long* keys, int cap,
                             unsigned long long key) {
   int h = (int)(mix64(key) & (unsigned long long)(cap - 1));
   for (int probe = 0; probe < cap; ++probe) {
-    const unsigned long long prev = atomicCAS(keys + h, kEmptyKey, key);
+    // a plain load first: most slots share a few masks, whose entries are
+    // taken long before most inserts arrive -- no atomic on those
+    unsigned long long prev = keys[h];
+    if (prev == kEmptyKey) prev = atomicCAS(keys + h, kEmptyKey, key);
     if (prev == kEmptyKey || prev == key) return h;
     h = (h + 1) & (cap - 1);
   }
@@ -157,16 +161,32 @@ __global__ __launch_bounds__(256) void kl_assign_kernel(
     const unsigned long long* __restrict__ keys, int cap, int* __restrict__ ids,
     unsigned long long* __restrict__ pool_mask, int pool_cap,
     int* __restrict__ counters, int D) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= cap) return;
-  const unsigned long long k = keys[i];
-  if (k != kEmptyKey && ids[i] < 0) {
-    const int id = atomicAdd(counters, 1);
-    ids[i] = id;
-    if (id < pool_cap) pool_mask[id] = k;
-    // the most flagged directions among the new masks (the deletion levels)
-    atomicMax(counters + 5, D - __popcll(k));
+  // grid-stride over the table (a power of two >= 64: every wave's lanes
+  // take the same trips)
+  int lvl = 0;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i - lane() < cap;
+       i += gridDim.x * blockDim.x) {
+    const unsigned long long k = i < cap ? keys[i] : kEmptyKey;
+    const bool fresh = k != kEmptyKey && ids[i] < 0;
+    // ids: one atomic per wavefront (the pool's order is immaterial: every
+    // entry is decomposed on its own, sf_get_fit_pool callers sort by mask)
+    const unsigned long long nb = __ballot(fresh);
+    if (nb == 0ull) continue;  // wave-uniform: most of the table is empty
+    int base = 0;
+    if (lane() == 0) base = atomicAdd(counters, __popcll(nb));
+    base = __shfl(base, 0);
+    if (fresh) {
+      const int id = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(nb >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)nb, 0));
+      ids[i] = id;
+      if (id < pool_cap) pool_mask[id] = k;
+      lvl = max(lvl, D - __popcll(k));
+    }
   }
+  // the most flagged directions among the new masks (the deletion levels):
+  // one atomic per wavefront
+  for (int o = 32; o > 0; o >>= 1) lvl = max(lvl, __shfl_xor(lvl, o));
+  if (lane() == 0 && lvl > 0) atomicMax(counters + 5, lvl);
 }
 
 // 3. subset bases of the masks numbered [counters[1], counters[0]):
@@ -1254,7 +1274,7 @@ static int number_and_decompose(sf_ctx* ctx, int* n_slow, int* n_nonuniform) {
   SF_HIP(hipMemsetAsync(ctx->d_counters + 5, 0, sizeof(int), ctx->stream));
   const int cap = (int)ctx->table_cap;
   const int old_cap = (int)ctx->pool_cap;
-  hipLaunchKernelGGL(kl_assign_kernel, dim3((cap + 255) / 256), dim3(256), 0,
+  hipLaunchKernelGGL(kl_assign_kernel, dim3(std::min((cap + 255) / 256, 8192)), dim3(256), 0,
                      ctx->stream, ctx->d_keys, cap, ctx->d_ids,
                      ctx->d_pool_mask, old_cap, ctx->d_counters, ctx->D);
   SF_HIP(hipGetLastError());
