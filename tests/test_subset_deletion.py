@@ -118,3 +118,29 @@ def test_deletions_match_lapack_on_the_config5_basis(k):
         gaps = np.array([np.min(np.abs(np.delete(l2, r) - l2[r])) for r in range(len(l2))])
         err = np.abs(Y * sg - V2).max(axis=0)
         assert np.max(err * gaps / lmax) <= 1e-12
+
+
+def test_ancestor_start_equals_the_chain():
+    """SF_OPT_FIT_SUBSET_DELETION = 1 starts a mask from its nearest
+    decomposed ancestor's pool entry (columns by |mu| descending, re-sorted
+    into ascending order by the kernel): an exact permutation of the state
+    the chain from the global basis has after the ancestor's deletions, so
+    the remaining deletions give the same bits (mode 2 is the chain)."""
+    from ska_sdp_screen_fitting_amd import geometry
+    from ska_sdp_screen_fitting_amd.synthetic import make_solutions
+    s = make_solutions(n_ant=2, n_time=1, n_freq=1, n_dir=20)
+    pp, _, _ = geometry.piercepoints(s.dir_radec)
+    c, _, _ = okl.calculate_svd(pp, 100.0, 5.0 / 3.0)
+    lam, U = np.linalg.eigh(c)
+    flagged = [17, 9, 4]                   # deleted in this (descending) order
+    keep = set(range(20)) - set(flagged)
+    mu, Y = subset_basis(lam, U, keep)     # the chain
+    # the ancestor: the mask with its lowest flagged direction unflagged
+    pa, Ya = subset_basis(lam, U, keep | {4})
+    order = np.lexsort((np.arange(pa.size), -np.abs(pa)))  # the pool entry
+    ent_l, ent_u = pa[order], Ya[:, order]
+    asc = np.lexsort((np.arange(ent_l.size), ent_l))       # back to ascending
+    l0, U0 = ent_l[asc], ent_u[:, asc]
+    assert np.array_equal(l0, pa) and np.array_equal(U0, Ya)
+    mu2, Y2 = delete(l0, U0, 4)            # row 4: every direction below 4 kept
+    assert np.array_equal(mu2, mu) and np.array_equal(Y2, Y)
