@@ -706,6 +706,9 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
   using G = Group<SPW>;
   using M = FitMath<!SLOW>;
   constexpr bool NI = !SLOW;
+  // mat-vec loops: four terms' loads in flight, the sums still in order (the
+  // same bits); the lean layout only (the general one would spill)
+  constexpr int kMatVecUnroll = LEAN ? 4 : 1;
   const int l = G::lane();
   const int n = B.n;
   double* v0 = L.vec;
@@ -731,6 +734,7 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
   lds_sync();
   double a1 = 0.0, a2 = 0.0;
   if (l < K) {
+#pragma unroll kMatVecUnroll
     for (int p = 0; p < n; ++p) {
       const double u = B.U[p * B.ld + l];
       a1 += u * v0[p];
@@ -802,6 +806,7 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
   double screen = 0.0;
   if (l < n) {
     double cre = 0.0, cim = 0.0;
+#pragma unroll kMatVecUnroll
     for (int k = 0; k < K; ++k) {
       const double u = B.U[l * B.ld + k];
       cre += u * v0[k];
@@ -815,6 +820,7 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
   // s_hat = U^T screen; white = U Lambda^+ s_hat; C white = U (Lambda Lambda^+) s_hat
   if (l < n) {
     double sh = 0.0;
+#pragma unroll kMatVecUnroll
     for (int p = 0; p < n; ++p) sh += B.U[p * B.ld + l] * v2[p];
     const double lm = B.lam[l];
     const bool keep = fabs(lm) > kAtol;
@@ -824,6 +830,7 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
   lds_sync();
   double white = 0.0, cw = 0.0;
   if (l < n) {
+#pragma unroll kMatVecUnroll
     for (int r = 0; r < n; ++r) {
       const double u = B.U[l * B.ld + r];
       white += u * v0[r];
@@ -867,6 +874,7 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
   lds_sync();
   if (l < D) {
     double sh = 0.0;
+#pragma unroll kMatVecUnroll
     for (int p = 0; p < D; ++p) sh += L.U[p * ld + l] * v2[p];
     const double lm = L.lam[l];
     v0[l] = fabs(lm) > kAtol ? sh / lm : 0.0;
@@ -874,6 +882,7 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
   lds_sync();
   double wa = 0.0;
   if (l < D)
+#pragma unroll kMatVecUnroll
     for (int r = 0; r < D; ++r) wa += L.U[l * ld + r] * v0[r];
   lds_sync();
   white_d = wa;
