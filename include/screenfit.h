@@ -195,13 +195,15 @@ int sf_device_cus(sf_ctx* ctx, int* n_cu);
  * bits (the rotations and their per-element arithmetic do not depend on how
  * a round's column pairs are split over the waves). */
 #define SF_OPT_FIT_EIG_WAVES 17
-/* SF_OPT_FIT_SUBSET_DELETION = 1 (default): the flagged-direction subset
- * bases by secular-equation deletions (Loewner-corrected vectors), one per
- * flagged direction, each mask starting from its nearest already
- * decomposed ancestor in the mask table (the mask with its lowest flagged
- * directions unflagged; the global basis when none is), the Jacobi solve
- * only for the masks the deletions cannot separate; 2 = the same deletions,
- * every mask from the global basis; 0 = the Jacobi solve for every mask. */
+/* SF_OPT_FIT_SUBSET_DELETION: the flagged-direction subset bases by
+ * secular-equation deletions (Loewner-corrected vectors), one per flagged
+ * direction, the Jacobi solve only for the masks the deletions cannot
+ * separate.  3 = each mask starts from its nearest ancestor in the mask
+ * table that the deletions built (the mask with its lowest flagged
+ * directions unflagged; the global basis when none is), one launch per
+ * number of flagged directions; 2 = every mask from the global basis, one
+ * launch; 1 (default) = 3 for a fit pass with many new masks, else 2;
+ * 0 = the Jacobi solve for every mask.  1, 2 and 3 write the same bits. */
 #define SF_OPT_FIT_SUBSET_DELETION 18
 #define SF_EVAL_KERNEL_AUTO 0
 #define SF_EVAL_KERNEL_TILE 1

@@ -238,8 +238,8 @@ int sf_set_option(sf_ctx* ctx, int option, int value) {
       ctx->eval_wg_waves = value;
       return SF_OK;
     case SF_OPT_FIT_SUBSET_DELETION:
-      SF_REQUIRE(value >= 0 && value <= 2, SF_EINVAL,
-                 "SF_OPT_FIT_SUBSET_DELETION must be 0, 1 or 2");
+      SF_REQUIRE(value >= 0 && value <= 3, SF_EINVAL,
+                 "SF_OPT_FIT_SUBSET_DELETION must be 0, 1, 2 or 3");
       ctx->fit_subset_deletion = (int)value;
       return SF_OK;
     case SF_OPT_FIT_EIG_WAVES:

@@ -149,6 +149,29 @@ int pick_eval_kernel(const sf_ctx* ctx, bool gain, unsigned flags,
   const bool lds_ok = !gain && (flags & SF_EVAL_FAST_SINCOS) &&
                       (ctx->n_pix % 4 == 0) && out_aligned16;
   const int opt = ctx->eval_kernel;
+  if (gain) {
+    // round 6: gain screens on the LDS-staged kernels whose three-plane tile
+    // fits LDS (LDS16's 1024-pixel run does not: LDS16H instead), fast
+    // epilogue, float4-aligned output, up to kGainLdsMaxKS k-steps including
+    // any zero padding
+    const bool glds = (flags & SF_EVAL_FAST_SINCOS) && ctx->n_pix % 4 == 0 &&
+                      out_aligned16 && ctx->ksteps + ctx->eval_ks_pad <= kGainLdsMaxKS;
+    switch (opt) {
+      case SF_EVAL_KERNEL_LDS4:
+      case SF_EVAL_KERNEL_LDS8:
+      case SF_EVAL_KERNEL_LDS8H:
+      case SF_EVAL_KERNEL_LDS16H:
+        return glds ? opt : SF_EVAL_KERNEL_TILE;
+      case SF_EVAL_KERNEL_LDS16:
+        return glds ? SF_EVAL_KERNEL_LDS16H : SF_EVAL_KERNEL_TILE;
+      case SF_EVAL_KERNEL_TILE3:
+        return opt;
+      case SF_EVAL_KERNEL_AUTO:
+        return glds ? kGainLdsAuto : SF_EVAL_KERNEL_TILE;
+      default:
+        return SF_EVAL_KERNEL_TILE;
+    }
+  }
   // the integer-digit contraction (phase D >= 45) runs on the register tile,
   // the SHB tile (pixel digits in LDS) and the LDS-staged kernels (same bits)
   const bool ic = eval_int_applies(ctx, gain, flags, out_aligned16);

@@ -99,6 +99,10 @@ __device__ __forceinline__ void rev_reduce_n(float (&f)[N], const double (&rev)[
 constexpr double kRevMagic = 1572864.0;          // 1.5 * 2^20
 constexpr float kTwoM32 = 2.3283064365386963e-10f;  // 2^-32
 constexpr int kMagicMaxKS = 11;
+// gain screens on the LDS-staged kernels (round 6): up to this many k-steps,
+// and the shape the auto choice takes
+constexpr int kGainLdsMaxKS = 11;
+constexpr int kGainLdsAuto = SF_EVAL_KERNEL_TILE;
 
 template <int KS>
 __device__ __forceinline__ bool group_rev_safe(const double (&af)[KS], double thr) {
@@ -863,27 +867,44 @@ __global__ __launch_bounds__(64 * NWV, MINW) void kl_eval_kernel(
 // TPW = MFMA tiles per wave: 4 (the wave owns a whole 64-pixel block, as in
 // the register-tile kernel) or 2 (two waves share a block, each holding half
 // of its Cpix fragments -- half the registers, for large D).
-template <int NW, int TPW>
+// GAIN (round 6): the tile holds three fp32 planes per value -- the reduced
+// phase, log2 A_XX and log2 A_YY, exactly the values the register tile feeds
+// to v_sin / v_cos and v_exp_f32 -- and the store waves run the whole gain
+// epilogue.  Two buffers (one barrier per group) while they fit the 160 KiB
+// of LDS, else one buffer and a second barrier once every wave has read it.
+template <int NW, int TPW, bool GAIN = false>
 struct EvalLds {
   static constexpr int kWavesPerBlock = kTiles / TPW;
   static constexpr int kRun = kWavePix * NW / kWavesPerBlock;  // pixels per workgroup
   static constexpr int kStride = kRun + 4;      // padded LDS row (floats)
   static constexpr int kSlotsPerWave = 16 / NW;
   static constexpr int kChunks = kRun / 256;    // 1-KiB store runs per plane
+  static constexpr int kPlanes = GAIN ? 3 : 1;  // fp32 values per (slot, pixel)
+  static constexpr int kBufBytes = kPlanes * 16 * kStride * 4;
+  static constexpr int kCsumBytes = 2 * 16 * 16 * 4;
+  // gain: one buffer always (the 1-KiB-run shapes then fit 2-3 workgroups
+  // per CU instead of 1: double-buffered, every SIMD of the CU ran its
+  // contraction and its stores in lockstep, 0.40-0.54 of 8 TB/s)
+  static constexpr int kBufs = !GAIN && 2 * kBufBytes + kCsumBytes <= 163840 ? 2 : 1;
+  static constexpr bool kFits = kBufs * kBufBytes + kCsumBytes <= 163840;
   static_assert(kRun % 256 == 0 && 16 % NW == 0, "bad LDS eval shape");
 };
 
-template <int KS, int NW, int TPW, bool NT, bool IC = false>
+template <int KS, int NW, int TPW, bool NT, bool IC = false, bool GAIN = false>
 __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
-    const double* __restrict__ cfrag, const double* __restrict__ coef, int D,
+    const double* __restrict__ cfrag, const double* __restrict__ coef,
+    const double* __restrict__ coef_xx, const double* __restrict__ coef_yy, int D,
     int ks_real, int64_t S, int64_t P, int64_t n_pb, int64_t n_sc,
     int chunk_groups, float* __restrict__ out, int64_t ring, int64_t ring_base,
     unsigned flags,
     int sleep, unsigned* __restrict__ sums, double rev_thr, DigArgs dg) {
-  using L = EvalLds<NW, TPW>;
+  using L = EvalLds<NW, TPW, GAIN>;
+  static_assert(L::kFits, "LDS eval shape exceeds 160 KiB");
+  static_assert(!(IC && GAIN), "integer contraction: phase screens");
   // IC: the integer-digit contraction (kl_eval_int.h) feeds the same LDS
-  // tile with the same reduced phases as the register tile's IC variant
-  __shared__ float tile[2][16][L::kStride];
+  // tile with the same reduced phases as the register tile's IC variant;
+  // GAIN: planes [1] / [2] hold log2 A_XX / A_YY
+  __shared__ float tile[L::kBufs][L::kPlanes][16][L::kStride];
   // checksums: slot sums of up to 16 groups per half ([half][group % 16]
   // [row]); wave 0 adds a half's 256 consecutive slots with 4 64-lane
   // atomics once the next half has begun, instead of one atomic per (wave,
@@ -940,7 +961,8 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
       const int64_t s0 = slot_base + (int64_t)g * 16;
       if (s0 >= S) break;  // uniform per workgroup
       ng_done = g + 1;
-      float(*buf)[L::kStride] = tile[g & 1];
+      const int bi = L::kBufs == 2 ? (g & 1) : 0;
+      float(*buf)[L::kStride] = tile[bi][0];
       // ---- contraction: 16 slots x this wave's 64 pixels
       if constexpr (IC) {
         // integer digits; rows the digits cannot carry (bit 4 (l >> 4) + r)
@@ -1004,7 +1026,15 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
       const bool magic = ks_real <= kMagicMaxKS;
       const double a0 = magic ? kRevMagic : 0.0;
       const bool safe = magic && group_rev_safe<KS>(af, rev_thr);
+      // gain: the XX / YY log-amplitude coefficients scaled by log2(10), as
+      // the register tile's fast path (kLog2of10)
+      double ax[GAIN ? KS : 1], ay[GAIN ? KS : 1];
+      if constexpr (GAIN) {
+        load_coef<KS>(ax, coef_xx, s0, S, D, l, kLog2of10);
+        load_coef<KS>(ay, coef_yy, s0, S, D, l, kLog2of10);
+      }
       v4d acc[TPW];
+      v4d accx[GAIN ? TPW : 1], accy[GAIN ? TPW : 1];
 #pragma unroll
       for (int t = 0; t < TPW; ++t) acc[t] = v4d{a0, a0, a0, a0};
       if constexpr (kEnergyDiag == 3) {
@@ -1012,6 +1042,10 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
         // stores stay)
 #pragma unroll
         for (int t = 0; t < TPW; ++t) acc[t] = v4d{af[0], af[0], bf[0][t], bf[0][t]};
+        if constexpr (GAIN) {
+#pragma unroll
+          for (int t = 0; t < TPW; ++t) accx[t] = accy[t] = acc[t];
+        }
       } else {
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk)
@@ -1020,20 +1054,60 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
           acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[kk], bf[kk][t],
                                                         acc[t], 0, 0, 0);
       }
+      const int col = wblk * kWavePix + (l & 15) * kTiles + t0;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float red[TPW];
         double rv[TPW];
 #pragma unroll
         for (int t = 0; t < TPW; ++t) rv[t] = acc[t][r];
-        rev_reduce_magic<TPW>(red, rv, safe, a0, scrub);
-        float* dst = &buf[acc_row(l, r)][wblk * kWavePix + (l & 15) * kTiles + t0];
+        // gain screens scrub the products (the store side), not the phase
+        rev_reduce_magic<TPW>(red, rv, safe, a0, !GAIN && scrub);
+        float* dst = &buf[acc_row(l, r)][col];
         if (TPW == 4)
           *reinterpret_cast<v4f*>(dst) = v4f{red[0], red[1], red[2 % TPW], red[3 % TPW]};
         else
           *reinterpret_cast<v2f*>(dst) = v2f{red[0], red[1 % TPW]};
       }
+      if constexpr (GAIN && kEnergyDiag != 3) {
+        // the log-amplitude contractions after the phase one is in LDS (its
+        // accumulators free again): the same products in the same order per
+        // accumulator as the register tile (kl_eval_kernel GAIN), the same bits
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+          accx[t] = v4d{0.0, 0.0, 0.0, 0.0};
+          accy[t] = v4d{0.0, 0.0, 0.0, 0.0};
+        }
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+          for (int t = 0; t < TPW; ++t) {
+            accx[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ax[kk], bf[kk][t], accx[t], 0, 0, 0);
+            accy[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ay[kk], bf[kk][t], accy[t], 0, 0, 0);
+          }
       }
+      if constexpr (GAIN) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          // log2 A rounded to float: amp2f's argument
+          float lx[TPW], ly[TPW];
+#pragma unroll
+          for (int t = 0; t < TPW; ++t) {
+            lx[t] = (float)accx[t][r];
+            ly[t] = (float)accy[t][r];
+          }
+          float* dx = &tile[bi][GAIN ? 1 : 0][acc_row(l, r)][col];
+          float* dy = &tile[bi][GAIN ? 2 : 0][acc_row(l, r)][col];
+          if (TPW == 4) {
+            *reinterpret_cast<v4f*>(dx) = v4f{lx[0], lx[1 % TPW], lx[2 % TPW], lx[3 % TPW]};
+            *reinterpret_cast<v4f*>(dy) = v4f{ly[0], ly[1 % TPW], ly[2 % TPW], ly[3 % TPW]};
+          } else {
+            *reinterpret_cast<v2f*>(dx) = v2f{lx[0], lx[1 % TPW]};
+            *reinterpret_cast<v2f*>(dy) = v2f{ly[0], ly[1 % TPW]};
+          }
+        }
+      }
+      }  // fp64 contraction
       for (int z = 0; z < sleep; ++z) __builtin_amdgcn_s_sleep(1);
       __syncthreads();
       // every wave wrote its sums of groups < g before this barrier
@@ -1097,7 +1171,103 @@ __global__ __launch_bounds__(64 * NW) void kl_eval_lds_kernel(
           if (l == 0) csum[(g >> 4) & 1][g & 15][row] = tot;
         }
       };
-      if (be) {
+      if constexpr (GAIN) {
+        // this wave's values of the group, read before any is used: with one
+        // buffer the next group's writes wait at a second barrier for every
+        // wave's reads, not for its stores
+        v4f rph[L::kSlotsPerWave][L::kChunks], rlx[L::kSlotsPerWave][L::kChunks],
+            rly[L::kSlotsPerWave][L::kChunks];
+#pragma unroll
+        for (int j = 0; j < L::kSlotsPerWave; ++j) {
+          const int row = w * L::kSlotsPerWave + j;
+#pragma unroll
+          for (int c = 0; c < L::kChunks; ++c) {
+            rph[j][c] = *reinterpret_cast<const v4f*>(&tile[bi][0][row][c * 256 + 4 * l]);
+            rlx[j][c] = *reinterpret_cast<const v4f*>(&tile[bi][GAIN ? 1 : 0][row][c * 256 + 4 * l]);
+            rly[j][c] = *reinterpret_cast<const v4f*>(&tile[bi][GAIN ? 2 : 0][row][c * 256 + 4 * l]);
+          }
+        }
+        if constexpr (L::kBufs == 1) __syncthreads();
+        // the register tile's gain epilogue (fast path) value for value:
+        // A = v_exp_f32 of log2 A, fp32 A x cos / sin, per-value NaN scrub
+        // of the products (screen.py:368-378), byte swap, 4 distinct planes
+        auto gain_out = [&](int j, auto be_tag) {
+          constexpr bool kBE = decltype(be_tag)::value;
+          const int row = w * L::kSlotsPerWave + j;
+          const int64_t s = s0 + row;
+          if (s >= S) return;  // uniform per wave
+          const int64_t so = (uint32_t)(s + ring_base) % (uint32_t)ring;
+          float* o = out + (so * 4) * P + pix0 + 4 * l;
+          unsigned cs = 0u;
+          // one 1-KiB chunk per plane at a time (fewer live registers)
+#pragma unroll
+          for (int c = 0; c < L::kChunks; ++c) {
+            float pv[4][4];
+            bool bad = false;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              float sn, cn, xa, ya;
+              if constexpr (kEnergyDiag == 3) {
+                // energy diagnostic: stores only (no sincos / exp2)
+                sn = rph[j][c][e];
+                cn = -sn;
+                xa = rlx[j][c][e];
+                ya = rly[j][c][e];
+              } else {
+                sincos_rev(rph[j][c][e], sn, cn);
+                xa = __builtin_amdgcn_exp2f(rlx[j][c][e]);
+                ya = __builtin_amdgcn_exp2f(rly[j][c][e]);
+              }
+              pv[0][e] = xa * cn;
+              pv[1][e] = xa * sn;
+              pv[2][e] = ya * cn;
+              pv[3][e] = ya * sn;
+              bad |= __builtin_isunordered(pv[0][e], pv[1][e]) |
+                     __builtin_isunordered(pv[2][e], pv[3][e]);
+            }
+            if (scrub && __builtin_amdgcn_ballot_w64(bad) != 0) {
+#pragma unroll
+              for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                  if (isnan(pv[q][e])) pv[q][e] = (q & 1) ? 0.0f : 1.0f;
+            }
+            if (kBE) {
+#pragma unroll
+              for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) pv[q][e] = bswapf(pv[q][e]);
+            }
+            if (pix0 + c * 256 + 4 * l < P) {
+#pragma unroll
+              for (int q = 0; q < 4; ++q)
+                store4<NT>(o + q * P + c * 256, v4f{pv[q][0], pv[q][1], pv[q][2], pv[q][3]});
+              // checksum of the stored words (all four planes differ)
+              if (sums) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                  for (int e = 0; e < 4; ++e) cs += fbits(pv[q][e]);
+              }
+            }
+          }
+          if (sums) {
+            cs = row_sum16(cs);
+            const unsigned tot = (unsigned)__builtin_amdgcn_readlane((int)cs, 0) +
+                                 (unsigned)__builtin_amdgcn_readlane((int)cs, 16) +
+                                 (unsigned)__builtin_amdgcn_readlane((int)cs, 32) +
+                                 (unsigned)__builtin_amdgcn_readlane((int)cs, 48);
+            if (l == 0) csum[(g >> 4) & 1][g & 15][row] = tot;
+          }
+        };
+        if (be) {
+#pragma unroll
+          for (int j = 0; j < L::kSlotsPerWave; ++j) gain_out(j, std::true_type{});
+        } else {
+#pragma unroll
+          for (int j = 0; j < L::kSlotsPerWave; ++j) gain_out(j, std::false_type{});
+        }
+      } else if (be) {
 #pragma unroll
         for (int j = 0; j < L::kSlotsPerWave; ++j) slot_out(j, std::true_type{});
       } else {
@@ -1355,12 +1525,12 @@ inline DigArgs dig_args(const sf_ctx* ctx, int64_t off) {
   return dg;
 }
 
-template <int KS, int NW, int TPW>
-int launch_eval_lds(sf_ctx* ctx, const double* coef, int64_t S_all,
-                           float* out, int64_t ring, unsigned flags,
-                           unsigned* sums) {
+template <int KS, int NW, int TPW, bool GAIN = false>
+int launch_eval_lds(sf_ctx* ctx, const double* coef, const double* cxx,
+                    const double* cyy, int64_t S_all, float* out, int64_t ring,
+                    unsigned flags, unsigned* sums) {
   const int64_t P = ctx->n_pix;
-  const int64_t run = EvalLds<NW, TPW>::kRun;
+  const int64_t run = EvalLds<NW, TPW, GAIN>::kRun;
   const int64_t n_pb = (P + run - 1) / run;
   // Small grids (n_pb <= 64: 256^2 and below, pixel blocks dealt to the XCDs
   // interleaved): the shortest items whose Cpix reload (8 x 4 KS bytes per
@@ -1376,8 +1546,8 @@ int launch_eval_lds(sf_ctx* ctx, const double* coef, int64_t S_all,
   int64_t per = eval_launch_slots(ctx, n_pb, groups, 64 * NW);
   // the integer-digit contraction: per-launch slot digits (run_kdig), at
   // most kDigChunk slots per launch
-  const bool ic = eval_int_applies(ctx, false, flags,
-                                   (reinterpret_cast<uintptr_t>(out) & 15) == 0);
+  const bool ic = !GAIN && eval_int_applies(ctx, false, flags,
+                                            (reinterpret_cast<uintptr_t>(out) & 15) == 0);
   if (ic) {
     const int64_t gs = 16 * (int64_t)groups;
     const int64_t cap = kDigChunk < gs ? gs : (kDigChunk / gs) * gs;
@@ -1390,6 +1560,8 @@ int launch_eval_lds(sf_ctx* ctx, const double* coef, int64_t S_all,
   const int64_t n_sc = (S + 16 * groups - 1) / (16 * groups);
   const int64_t nblk = eval_grid(ctx, n_pb, n_sc, 64 * NW);
   const double* cb = coef + b * ctx->D;
+  const double* cxb = GAIN ? cxx + b * ctx->D : nullptr;
+  const double* cyb = GAIN ? cyy + b * ctx->D : nullptr;
   unsigned* sb = sums ? sums + b : nullptr;
   if (ic) {
     const int rc = run_kdig(ctx, cb, S);
@@ -1402,14 +1574,14 @@ int launch_eval_lds(sf_ctx* ctx, const double* coef, int64_t S_all,
   if (ctx->eval_xcd_map < 0 && (n_pb & 7) == 0 && n_pb / 8 <= 8)
     fl |= kEvalXcdInterleave;
   fl |= eval_band_flags(ctx, n_pb);
-#define SF_LAUNCH_LDS(N, I)                                                          \
-  hipLaunchKernelGGL((kl_eval_lds_kernel<KS, NW, TPW, N, I>), dim3((unsigned)nblk),     \
-                     dim3(64 * NW), 0, ctx->stream, ctx->d_cfrag, cb, ctx->D,           \
-                     ctx->ksteps, S, P, n_pb, n_sc, groups, out, ring, b % ring, fl,    \
+#define SF_LAUNCH_LDS(N, I)                                                             \
+  hipLaunchKernelGGL((kl_eval_lds_kernel<KS, NW, TPW, N, I, GAIN>), dim3((unsigned)nblk), \
+                     dim3(64 * NW), 0, ctx->stream, ctx->d_cfrag, cb, cxb, cyb, ctx->D,   \
+                     ctx->ksteps, S, P, n_pb, n_sc, groups, out, ring, b % ring, fl,      \
                      ctx->eval_sleep, sb, ctx->rev_thr, I ? dig_args(ctx, 0) : DigArgs{})
   // (the integer variant only where it can apply: D >= 45)
   if (ic) {
-    if constexpr (KS >= 12) {
+    if constexpr (KS >= 12 && !GAIN) {
       if (flags & SF_EVAL_NT_STORES) SF_LAUNCH_LDS(true, true);
       else SF_LAUNCH_LDS(false, true);
     }
@@ -1576,17 +1748,40 @@ int launch_eval_pick(sf_ctx* ctx, const double* coef, const double* cxx,
     if (v == SF_EVAL_KERNEL_SHB)
       return launch_eval_int_shb<KS>(ctx, coef, S, out, ring, flags, sums);
   }
+  // gain screens (round 6): the LDS-staged shapes whose three-plane tile
+  // fits LDS (pick_eval_kernel maps LDS16 to LDS16H), up to kGainLdsMaxKS
+  if (cxx != nullptr) {
+    if constexpr (KS <= kGainLdsMaxKS) {
+      switch (v) {
+        case SF_EVAL_KERNEL_LDS4:
+          return launch_eval_lds<KS, 4, 4, true>(ctx, coef, cxx, cyy, S, out, ring, flags, sums);
+        case SF_EVAL_KERNEL_LDS8:
+          return launch_eval_lds<KS, 8, 4, true>(ctx, coef, cxx, cyy, S, out, ring, flags, sums);
+        case SF_EVAL_KERNEL_LDS8H:
+          return launch_eval_lds<KS, 8, 2, true>(ctx, coef, cxx, cyy, S, out, ring, flags, sums);
+        case SF_EVAL_KERNEL_LDS16H:
+          return launch_eval_lds<KS, 16, 2, true>(ctx, coef, cxx, cyy, S, out, ring, flags, sums);
+        default:
+          break;
+      }
+    }
+    // (pick_eval_kernel gives gain screens no other LDS-staged shape)
+    if (v != SF_EVAL_KERNEL_TILE && v != SF_EVAL_KERNEL_TILE3) {
+      set_error("sf_kl_eval_gain: no LDS-staged gain kernel for this shape");
+      return SF_EINVAL;
+    }
+  }
   switch (v) {
     case SF_EVAL_KERNEL_LDS4:
-      return launch_eval_lds<KS, 4, 4>(ctx, coef, S, out, ring, flags, sums);
+      return launch_eval_lds<KS, 4, 4>(ctx, coef, nullptr, nullptr, S, out, ring, flags, sums);
     case SF_EVAL_KERNEL_LDS8:
-      return launch_eval_lds<KS, 8, 4>(ctx, coef, S, out, ring, flags, sums);
+      return launch_eval_lds<KS, 8, 4>(ctx, coef, nullptr, nullptr, S, out, ring, flags, sums);
     case SF_EVAL_KERNEL_LDS16:
-      return launch_eval_lds<KS, 16, 4>(ctx, coef, S, out, ring, flags, sums);
+      return launch_eval_lds<KS, 16, 4>(ctx, coef, nullptr, nullptr, S, out, ring, flags, sums);
     case SF_EVAL_KERNEL_LDS8H:
-      return launch_eval_lds<KS, 8, 2>(ctx, coef, S, out, ring, flags, sums);
+      return launch_eval_lds<KS, 8, 2>(ctx, coef, nullptr, nullptr, S, out, ring, flags, sums);
     case SF_EVAL_KERNEL_LDS16H:
-      return launch_eval_lds<KS, 16, 2>(ctx, coef, S, out, ring, flags, sums);
+      return launch_eval_lds<KS, 16, 2>(ctx, coef, nullptr, nullptr, S, out, ring, flags, sums);
     case SF_EVAL_KERNEL_SHB:
       return launch_eval_shb<KS>(ctx, coef, S, out, ring, flags, sums);
     case SF_EVAL_KERNEL_TILE3:

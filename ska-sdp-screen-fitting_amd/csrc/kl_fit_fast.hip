@@ -282,7 +282,11 @@ __global__ __launch_bounds__(64 * NW) void kl_subset_eig_kernel(
 //     its own (found in the mask table; decomposed by an earlier call, or by
 //     this call's lower levels without falling back) -- so a mask whose
 //     parent is in the pool costs one deletion instead of one per flagged
-//     direction.  level 0: every new mask from the global basis.
+//     direction.  level 0: every new mask from the global basis.  Either
+//     way a mask's basis is bit for bit the chain's from the global basis:
+//     an ancestor is taken only if the chain built it (status 0; status is
+//     kept for every pool entry of the call, the host sets 1 before a pass's
+//     launches, so an entry the Jacobi built is never a start).
 __global__ __launch_bounds__(64) void kl_subset_secular_kernel(
     const double* __restrict__ g_u, const double* __restrict__ g_eig, int D,
     const unsigned long long* __restrict__ pool_mask, int pool_cap,
@@ -327,7 +331,9 @@ __global__ __launch_bounds__(64) void kl_subset_secular_kernel(
         if (a == full) break;
         const int h = table_find(keys, table_cap, a);
         const int pid = h >= 0 ? ids[h] : -1;
-        if (pid >= 0 && pid < pool_cap && (pid < first || status[pid] == 0)) {
+        // chain-built ancestors only (status 0, kept across the passes of
+        // the call): an entry the Jacobi decomposed is not the chain's bits
+        if (pid >= 0 && pid < pool_cap && status[pid] == 0) {
           anc = a;
           aid = pid;
           break;
@@ -1276,6 +1282,10 @@ __global__ __launch_bounds__(256) void kl_fill_mask_kernel(
   if (keys[i] != kEmptyKey && ids[i] >= lo) pool_mask[ids[i]] = keys[i];
 }
 
+// new masks of a pass from which SF_OPT_FIT_SUBSET_DELETION = 1 starts
+// deletions from ancestors (below it: one launch from the global basis)
+constexpr int kAncestorMinMasks = 8192;
+
 // number new masks, make sure the pool holds them, decompose them
 static int number_and_decompose(sf_ctx* ctx, int* n_slow, int* n_nonuniform) {
   SF_HIP(hipMemcpyAsync(ctx->d_counters + 1, ctx->d_counters, sizeof(int),
@@ -1305,7 +1315,11 @@ static int number_and_decompose(sf_ctx* ctx, int* n_slow, int* n_nonuniform) {
   if (n_new > 0 && ctx->fit_subset_deletion && ctx->D <= 64) {
     // subset bases by deletions first (kl_subset_secular_kernel); the
     // Jacobi below takes the masks it left (status 1)
-    SF_TRYF(grow(&ctx->d_pool_status, ctx->pool_status_cap, (size_t)cnt[0]));
+    // (the status of every pool entry of the call is kept: a later pass's
+    // masks take an earlier pass's entries as ancestors only if the chain
+    // built them; the stream was synchronised above, so the copy is safe)
+    SF_TRYF(grow(&ctx->d_pool_status, ctx->pool_status_cap, ctx->pool_cap, true));
+    SF_HIP(hipMemsetAsync(ctx->d_pool_status + cnt[1], 1, (size_t)n_new, ctx->stream));
     const int D = ctx->D;
     const int ldd = D | 1;
     const size_t shm = (size_t)2 * D * ldd * sizeof(double) + 6 * 64 * sizeof(double) +
@@ -1314,10 +1328,19 @@ static int number_and_decompose(sf_ctx* ctx, int* n_slow, int* n_nonuniform) {
       SF_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&kl_subset_secular_kernel),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
     const int blocks = n_new < 16384 ? n_new : 16384;
-    // option 1: levels 1 .. (most flagged directions), each mask from its
-    // nearest decomposed ancestor; 2: one launch, every mask from the
-    // global basis
-    const int levels = ctx->fit_subset_deletion == 2 ? 0 : cnt[5];
+    // levels 1 .. (most flagged directions), each mask from its nearest
+    // decomposed ancestor (option 3, and option 1 -- the default -- when the
+    // pass has kAncestorMinMasks new masks or more), or one launch, every
+    // mask from the global basis (option 2, and option 1 below that count):
+    // the same bits either way.  The level launches are serial, one per
+    // level; they pay off where the deletions they save are many (config 5:
+    // ~113 k masks, 229 -> 192 ms per fit) and cost where the masks are few
+    // and deep (the gain step's amplitude fit: block flags, up to D - 1
+    // flagged directions per mask, ~31 level launches per step: 10.4 ->
+    // 18.7 ms per step)
+    const bool anc = ctx->fit_subset_deletion == 3 ||
+                     (ctx->fit_subset_deletion == 1 && n_new >= kAncestorMinMasks);
+    const int levels = anc ? cnt[5] : 0;
     for (int lv = levels > 0 ? 1 : 0; lv <= levels; ++lv) {
       hipLaunchKernelGGL(kl_subset_secular_kernel, dim3(blocks), dim3(64), shm, ctx->stream,
                          ctx->d_u, ctx->d_eig, D, ctx->d_pool_mask, (int)ctx->pool_cap,

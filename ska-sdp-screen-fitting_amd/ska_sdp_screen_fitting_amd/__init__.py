@@ -2,7 +2,8 @@
 ska-sdp-screen-fitting).  Python host code over the C ABI of libscreenfit.so
 (hand-written HIP for gfx950); see DESIGN.md."""
 
-from ._lib import Context, ScreenFitError, get_context, load_library  # noqa: F401
+from ._lib import (Context, ScreenFitError, get_context, load_library,  # noqa: F401
+                   private_context)
 
 __version__ = "0.1.0"
 

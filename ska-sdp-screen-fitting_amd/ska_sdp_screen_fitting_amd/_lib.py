@@ -4,6 +4,7 @@ There is no fallback: if the library is missing or no gfx950 device is
 usable, every compute entry point raises :class:`ScreenFitError`.
 """
 
+import contextlib
 import ctypes
 import os
 import threading
@@ -427,13 +428,42 @@ class Context:
 
 
 _contexts = {}
+_ctx_lock = threading.Lock()
 
 
 def get_context(device=0):
     """Process-wide context per device (bound to torch's current stream by
-    the callers that use torch)."""
-    ctx = _contexts.get(device)
+    the callers that use torch).  Its basis, grid, options and scratch are
+    shared by every holder: for a single-threaded caller (the bench, the
+    tests) -- the product paths take a ``private_context`` instead."""
+    with _ctx_lock:
+        ctx = _contexts.get(device)
+        if ctx is None:
+            ctx = Context(device)
+            _contexts[device] = ctx
+    return ctx
+
+
+_idle = {}
+
+
+@contextlib.contextmanager
+def private_context(device=0):
+    """A context this block holds alone: taken from the device's idle list
+    (or created) and returned to it on exit, so a caller's set_basis / fit /
+    tess_fill sequence never sees a basis, grid or scratch buffer another
+    thread set meanwhile.  The reference's counterpart is its module-global
+    state per worker process (stationscreen.py:918-919, kl_screen.py:223-226);
+    there one screen at a time per process, here any number of threads, one
+    context each while they run (at most as many contexts as ever ran
+    concurrently)."""
+    with _ctx_lock:
+        idle = _idle.setdefault(device, [])
+        ctx = idle.pop() if idle else None
     if ctx is None:
         ctx = Context(device)
-        _contexts[device] = ctx
-    return ctx
+    try:
+        yield ctx
+    finally:
+        with _ctx_lock:
+            _idle[device].append(ctx)

@@ -41,8 +41,7 @@ def read_patch_names(skymodel_filename):
 class KLEvaluator:
     """Device state for evaluating KL screens on one grid.  Owns its sf_ctx:
     the basis and pixel grid it sets stay put whatever other screens or the
-    fit (which uses the process-wide context of ``get_context``) set
-    meanwhile."""
+    fit (which takes a ``private_context`` per call) set meanwhile."""
 
     def __init__(self, piercepoints, r_0, beta, x_coord, y_coord, device=0):
         import torch

@@ -16,7 +16,7 @@ import logging
 import numpy as np
 
 from . import geometry
-from ._lib import SF_SCREEN_AMPLITUDE, SF_SCREEN_PHASE, SF_SCREEN_TEC, get_context
+from ._lib import SF_SCREEN_AMPLITUDE, SF_SCREEN_PHASE, SF_SCREEN_TEC, private_context
 
 log = logging.getLogger("ska_sdp_screen_fitting_amd.stationscreen")
 
@@ -46,9 +46,10 @@ def _device_fit(phase, weight, pp, st_order, screen_type, niter, nsigma,
     import torch
 
     T, F, A, D = phase.shape
-    ctx = get_context(device)
     dev = torch.device("cuda", device)
-    with torch.cuda.device(dev):
+    # a context of its own for the basis + fit sequence: another thread's
+    # fit or screen cannot re-base it between the two
+    with private_context(device) as ctx, torch.cuda.device(dev):
         ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
         ctx.set_basis(pp, r_0, beta)
         ph = torch.from_numpy(np.ascontiguousarray(phase, np.float64)).to(dev)

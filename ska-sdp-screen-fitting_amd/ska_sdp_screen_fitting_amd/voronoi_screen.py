@@ -21,7 +21,7 @@ from PIL import Image, ImageDraw
 from scipy.spatial import Voronoi
 
 from . import fits, geometry
-from ._lib import SF_EVAL_BIG_ENDIAN, SF_EVAL_NAN_SCRUB, get_context
+from ._lib import SF_EVAL_BIG_ENDIAN, SF_EVAL_NAN_SCRUB, private_context
 from .h5parm import H5parm, get_reference_station
 from .screen import Screen
 
@@ -276,8 +276,9 @@ class VoronoiScreen(Screen):
         dev, lab = self._device()
         ny, nx = self.data_rasertize_template.shape
         S, D = ph_dev.shape
-        ctx = get_context(self.device)
-        with torch.cuda.device(dev):
+        # the fill's scratch (table, smoothing buffers) is the context's: a
+        # context of its own per call
+        with private_context(self.device) as ctx, torch.cuda.device(dev):
             ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
             ctx.tess_fill(lab, nx, ny, ph_dev, D, S, out_dev, amp_xx=amp_xx,
                           amp_yy=amp_yy, smooth_pix=smooth_pix, flags=flags)

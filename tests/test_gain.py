@@ -276,6 +276,113 @@ def test_gain_eval_finite_groups_and_scrub(gain, fast):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n_dir,grid", [(20, 256), (7, 128), (24, 60), (3, 40),
+                                        (44, 32), (50, 64)])
+def test_gain_eval_kernels_agree(n_dir, grid):
+    """Every gain evaluation kernel -- the register tile and the LDS-staged
+    shapes (round 6: LDS4 / LDS8 / LDS8H / LDS16H, LDS16 mapped to LDS16H)
+    -- writes the same bits as the register tile, with plain, non-temporal
+    and big-endian stores, walking workgroups, both XCD maps, short work
+    items, and through sf_kl_eval_sums (equal per-slot checksums).  Ragged
+    slot count (45: a partial 16-slot group), grids that are not a multiple
+    of the LDS store run, NaN / Inf phase and amplitude coefficients (the
+    scrubbed products), large amplitudes; D = 50 (past kGainLdsMaxKS) runs
+    the register tile under every setting; the tile output is within the
+    fast-path tolerance of fp64 numpy."""
+    from ska_sdp_screen_fitting_amd import geometry
+    from ska_sdp_screen_fitting_amd._lib import (
+        EVAL_KERNEL_NAMES, SF_EVAL_BIG_ENDIAN, SF_EVAL_FAST_SINCOS,
+        SF_EVAL_KERNEL_AUTO, SF_EVAL_KERNEL_TILE, SF_EVAL_NAN_SCRUB,
+        SF_EVAL_NT_STORES, SF_OPT_EVAL_GROUPS, SF_OPT_EVAL_KERNEL,
+        SF_OPT_EVAL_MAX_BLOCKS, SF_OPT_EVAL_XCD_MAP)
+    from ska_sdp_screen_fitting_amd.synthetic import make_solutions
+    torch, dev = _torch_dev()
+    ctx = _ctx(torch, dev)
+    s = make_solutions(n_ant=2, n_time=2, n_freq=1, n_dir=n_dir, seed=4)
+    pp, mra, mdec = geometry.piercepoints(s.dir_radec)
+    cell = FIELD["width"] / (grid - 0.5)
+    x, y = geometry.grid_coords(FIELD["rad"], FIELD["dec"], FIELD["width"],
+                                cell, mra, mdec)
+    ctx.set_basis(pp)
+    ctx.set_grid(x, y)
+    rng = np.random.default_rng(n_dir * 7 + grid)
+    S = 45
+    ph = rng.normal(0, 0.01, (S, n_dir))
+    ph[20:30] *= 300.0                 # many turns: the exact reduction
+    ax = rng.normal(0, 0.002, (S, n_dir))
+    ay = rng.normal(0, 0.002, (S, n_dir))
+    # large amplitudes: |log2 A| up to 60 (finite in fp32)
+    cpix = okl.cpix_matrix(pp, x, y)
+    big = ax[33:40] @ cpix.T * np.log2(10.0)
+    ax[33:40] *= 60.0 / np.abs(big).max()
+    ph[9, n_dir // 2] = np.nan
+    ph[31, 0] = np.inf
+    ax[12, n_dir - 1] = np.nan         # XX planes scrubbed, YY kept
+    ay[41, 0] = np.inf
+    up = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (ph, ax, ay)]
+    base = SF_EVAL_NAN_SCRUB | SF_EVAL_FAST_SINCOS
+
+    def run(flags, sums=False):
+        out = torch.full((S, 4, grid, grid), -7.0, dtype=torch.float32, device=dev)
+        if sums:
+            cs = torch.zeros(S, dtype=torch.int32, device=dev)
+            ctx.eval_sums(up[0], S, out, cs, S, coef_xx=up[1], coef_yy=up[2],
+                          flags=flags)
+        else:
+            ctx.eval_gain(up[0], up[1], up[2], S, out, S, flags)
+        torch.cuda.synchronize()
+        o = out.cpu().numpy()
+        if flags & SF_EVAL_BIG_ENDIAN:
+            o = o.byteswap()
+        return (o, cs.cpu().numpy()) if sums else o
+
+    outs, sums = {}, {}
+    try:
+        for kv in sorted(EVAL_KERNEL_NAMES) + [SF_EVAL_KERNEL_AUTO]:
+            ctx.set_option(SF_OPT_EVAL_KERNEL, kv)
+            for extra in (0, SF_EVAL_NT_STORES, SF_EVAL_BIG_ENDIAN):
+                outs[(kv, extra)] = run(base | extra)
+            outs[(kv, "sums")], sums[kv] = run(base | SF_EVAL_NT_STORES, sums=True)
+            ctx.set_option(SF_OPT_EVAL_MAX_BLOCKS, 8)
+            outs[(kv, "walk")] = run(base)
+            ctx.set_option(SF_OPT_EVAL_MAX_BLOCKS, 0)
+            for xm in (0, 1):
+                ctx.set_option(SF_OPT_EVAL_XCD_MAP, xm)
+                outs[(kv, "xcd", xm)] = run(base)
+            ctx.set_option(SF_OPT_EVAL_XCD_MAP, -1)
+            ctx.set_option(SF_OPT_EVAL_GROUPS, 1)
+            outs[(kv, "g1")] = run(base)
+            ctx.set_option(SF_OPT_EVAL_GROUPS, 0)
+    finally:
+        ctx.set_option(SF_OPT_EVAL_KERNEL, SF_EVAL_KERNEL_AUTO)
+        ctx.set_option(SF_OPT_EVAL_MAX_BLOCKS, 0)
+        ctx.set_option(SF_OPT_EVAL_XCD_MAP, -1)
+        ctx.set_option(SF_OPT_EVAL_GROUPS, 0)
+    ref = outs[(SF_EVAL_KERNEL_TILE, 0)]
+    for k, o in outs.items():
+        assert np.array_equal(o.view(np.int32), ref.view(np.int32)), k
+    # the checksum is the sum mod 2^32 of each slot's stored words
+    want_sums = ref.reshape(S, -1).view(np.uint32).astype(np.uint64).sum(1) % 2 ** 32
+    for kv, cs in sums.items():
+        assert np.array_equal(cs.view(np.uint32), want_sums.astype(np.uint32)), kv
+    # scrubbed products: NaN phase -> all four planes 1 / 0; NaN log A_XX ->
+    # the XX planes
+    for k in (9, 31):
+        assert np.all(ref[k, 0::2] == 1.0) and np.all(ref[k, 1::2] == 0.0)
+    assert np.all(ref[12, 0] == 1.0) and np.all(ref[12, 1] == 0.0)
+    good = np.isfinite(ph).all(1) & np.isfinite(ax).all(1) & np.isfinite(ay).all(1)
+    L = np.log2(10.0)
+    phase = ph[good] @ cpix.T
+    lx, ly = ax[good] @ cpix.T * L, ay[good] @ cpix.T * L
+    want = np.stack([2 ** lx * np.cos(phase), 2 ** lx * np.sin(phase),
+                     2 ** ly * np.cos(phase), 2 ** ly * np.sin(phase)], 1)
+    ampl = np.maximum(1.0, np.stack([2 ** lx, 2 ** lx, 2 ** ly, 2 ** ly], 1))
+    lmax = np.maximum(np.abs(lx), np.abs(ly))[:, None, :]
+    err = np.abs(ref[good].reshape(want.shape) - want) / ampl
+    assert np.all(err <= 2e-6 + 1.2e-7 * lmax), err.max()
+
+
+@pytest.mark.gpu
 def test_make_aterm_image_gain_kl(tmp_path, gain):
     """make_aterm_image on a gain solution set (soltab "gain000" -> phase000
     + amplitude000), FITS cube vs the reference's make_matrix output."""

@@ -726,7 +726,7 @@ def test_fit_vs_oracle_on_bench_workload_sample(ctx, dev, T):
     assert not bad, bad[:12]
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [1, 2, 3])
 @pytest.mark.parametrize("name", ["synth50", "config5-density", "synth20", "fixture_kl"])
 def test_subset_deletion_bases_match_jacobi(ctx, dev, name, mode):
     """SF_OPT_FIT_SUBSET_DELETION: the subset bases by secular-equation
@@ -734,8 +734,9 @@ def test_subset_deletion_bases_match_jacobi(ctx, dev, name, mode):
     the same masks, eigenvalues to 1e-12 of |lambda|max, each eigenvector
     to the conditioning of its eigenvalue gap (sign free), and the fit's
     orders and flags identical, coefficients within 1e-9 of the golden.
-    mode 1 (the default): each mask from its nearest decomposed ancestor;
-    mode 2: every mask from the global basis."""
+    mode 3: each mask from its nearest ancestor the deletions built; mode 2:
+    every mask from the global basis; mode 1 (the default): 3 for a pass
+    with many new masks, else 2."""
     from ska_sdp_screen_fitting_amd._lib import SF_OPT_FIT_SUBSET_DELETION
     g = _wave_count_case(name) if name == "config5-density" else load_golden(name)
     ctx.set_option(SF_OPT_FIT_SUBSET_DELETION, 0)
@@ -801,7 +802,7 @@ def _deletion_edge_case(name):
                 ref_ant=okl.reference_station(s.weight), order=min(20, n_dir))
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [1, 2, 3])
 @pytest.mark.parametrize("name", ["heavy50", "d60", "d4", "lattice25"])
 def test_subset_deletion_edge_cases(ctx, dev, name, mode):
     """The deletion subset bases vs the Jacobi's at the kernel's edges
@@ -876,3 +877,88 @@ def test_subset_deletion_edge_cases(ctx, dev, name, mode):
     assert name == "d4" or not tie
     scale = max(1.0, np.abs(jac[0]).max())
     assert np.abs(dele[0] - jac[0])[keep].max() <= 1e-9 * scale
+
+
+@pytest.mark.parametrize("name", ["heavy50", "lattice25", "d4", "synth20"])
+def test_subset_deletion_modes_bit_identical(ctx, dev, name):
+    """The three deletion schedules write the same bits: from
+    ancestors (mode 3, one launch per level), from the global basis (mode
+    2) and the default (1), over three passes (niter 3, so later passes'
+    masks take earlier passes' pool entries as ancestors), also on the
+    lattice, where the Jacobi fallback builds some entries: an ancestor is
+    taken only if the deletion chain built it, so no mask's bits depend on
+    which pass or which other slots produced its parent."""
+    from ska_sdp_screen_fitting_amd._lib import SF_OPT_FIT_SUBSET_DELETION
+    g = load_golden(name) if name == "synth20" else _deletion_edge_case(name)
+    outs = {}
+    try:
+        for mode in (2, 3, 1):
+            ctx.set_option(SF_OPT_FIT_SUBSET_DELETION, mode)
+            outs[mode] = gpu_fit(ctx, dev, g, niter=3)
+            outs[(mode, "pool")] = ctx.fit_pool()
+    finally:
+        ctx.set_option(SF_OPT_FIT_SUBSET_DELETION, 1)
+    for mode in (3, 1):
+        for a, b in zip(outs[mode], outs[2]):
+            assert np.array_equal(a.view(np.uint8), b.view(np.uint8)), mode
+        ma, pa = outs[(mode, "pool")]
+        mb, pb = outs[(2, "pool")]
+        assert np.array_equal(ma, mb)
+        assert np.array_equal(pa.view(np.uint64), pb.view(np.uint64)), mode
+
+
+def _golden_soltab(g):
+    """A phase soltab + solset of a golden set, as stationscreen.run reads
+    them (h5parm.Soltab / Solset)."""
+    from ska_sdp_screen_fitting_amd.h5parm import Solset, Soltab
+    ss = Solset("sol000", list(g["ant_names"]), g["ant_pos"], list(g["dir_names"]),
+                g["dir_radec"])
+    st = Soltab("phase000", "phase", ["time", "freq", "ant", "dir"],
+                [g["times"], g["freqs"], list(g["ant_names"]), list(g["dir_names"])],
+                np.array(g["val"]), np.array(g["weight"]), solset=ss)
+    ss.soltabs["phase000"] = st
+    return st
+
+
+def test_threads_fit_on_private_contexts(dev):
+    """Two threads run stationscreen.run on different golden sets (synth20,
+    synth50: different bases) on one device, interleaved -- each call takes
+    a context of its own (_lib.private_context), so neither can re-base the
+    other between its set_basis and its fit (the round-5 r5x failure mode of
+    one shared context).  Every run matches its reference golden: orders and
+    flagged weights bit for bit, coefficients <= 1e-8."""
+    import threading
+    from ska_sdp_screen_fitting_amd import stationscreen
+    from ska_sdp_screen_fitting_amd._lib import get_context
+    goldens = {n: load_golden(n) for n in ("synth20", "synth50")}
+    # the process-wide context holds a third basis meanwhile
+    get_context(0).set_basis(load_golden("fixture_kl")["piercepoints"])
+    errors, done = [], {n: 0 for n in goldens}
+    start = threading.Barrier(len(goldens))
+
+    def worker(name):
+        g = goldens[name]
+        try:
+            start.wait()
+            for it in range(4):
+                st = _golden_soltab(g)
+                assert stationscreen.run(st, "phase_screen000", order=int(g["order"]),
+                                         ref_ant=int(g["ref_ant"])) == 0
+                ss = st.get_solset()
+                scr = ss.get_soltab("phase_screen000")
+                res = ss.get_soltab("phase_screen000resid")
+                np.testing.assert_array_equal(res.weight[..., 0], g["orders"])
+                np.testing.assert_array_equal(scr.weight, g["w_out"])
+                scale = max(1.0, np.abs(g["coef"]).max())
+                np.testing.assert_allclose(scr.val, g["coef"], rtol=0, atol=1e-8 * scale)
+                done[name] += 1
+        except Exception as e:  # noqa: BLE001 -- reported by the main thread
+            errors.append((name, repr(e)))
+
+    ths = [threading.Thread(target=worker, args=(n,)) for n in goldens]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=300)
+    assert not errors, errors
+    assert all(v == 4 for v in done.values()), done

@@ -121,8 +121,8 @@ def test_deletions_match_lapack_on_the_config5_basis(k):
 
 
 def test_ancestor_start_equals_the_chain():
-    """SF_OPT_FIT_SUBSET_DELETION = 1 starts a mask from its nearest
-    decomposed ancestor's pool entry (columns by |mu| descending, re-sorted
+    """SF_OPT_FIT_SUBSET_DELETION = 3 (and 1 on passes with many new masks)
+    starts a mask from its nearest chain-built ancestor's pool entry (columns by |mu| descending, re-sorted
     into ascending order by the kernel): an exact permutation of the state
     the chain from the global basis has after the ancestor's deletions, so
     the remaining deletions give the same bits (mode 2 is the chain)."""

@@ -37,6 +37,11 @@ ap.add_argument("--variants", default=",".join(
 ap.add_argument("--reps", type=int, default=7)
 ap.add_argument("--slots", type=int, default=102400,
                 help="slots per launch at 256^2 (scaled by 256^2/N^2)")
+ap.add_argument("--no-check", action="store_true",
+                help="skip the bitwise cross-check (energy-diagnostic builds)")
+ap.add_argument("--gain", action="store_true",
+                help="gain screens (sf_kl_eval_gain: phase + XX / YY log-amplitude "
+                     "coefficients, three contractions, four distinct planes)")
 args = ap.parse_args()
 
 dev = torch.device("cuda", 0)
@@ -96,7 +101,18 @@ for sh in args.shapes:
                    np.zeros(D)], 1)
     S = args.slots * (256 * 256) // (N * N)
     coef = torch.from_numpy(rng.normal(0, 0.01, (S, D))).to(dev)
+    if args.gain:
+        amps = tuple(torch.from_numpy(rng.normal(0, 0.002, (S, D))).to(dev)
+                     for _ in range(2))
+        coef = (coef,) + amps
     shapes.append((D, N, S, pp, coef))
+
+
+def run_eval(coef, S, out, ring, fl):
+    if args.gain:
+        ctx.eval_gain(coef[0], coef[1], coef[2], S, out, ring, fl)
+    else:
+        ctx.eval(coef, S, out, ring, fl)
 
 
 def select(D, N, pp):
@@ -106,16 +122,21 @@ def select(D, N, pp):
 
 
 # bitwise cross-check on a small ragged batch with a NaN coefficient
-for D, N, S, pp, coef in shapes:
+for D, N, S, pp, coef in ([] if args.no_check else shapes):
     select(D, N, pp)
     Sc = 37
-    cchk = coef[:Sc].clone()
-    cchk[5, min(3, D - 1)] = float("nan")
+    if args.gain:
+        cchk = tuple(c[:Sc].clone() for c in coef)
+        cchk[0][5, min(3, D - 1)] = float("nan")
+        cchk[1][7, 0] = float("nan")
+    else:
+        cchk = coef[:Sc].clone()
+        cchk[5, min(3, D - 1)] = float("nan")
     refs = {}
     for name, (kv, fl, opts) in variants.items():
         use(kv, opts)
         o = torch.full((Sc, 4, N, N), -7.0, dtype=torch.float32, device=dev)
-        ctx.eval(cchk, Sc, o, Sc, fl)
+        run_eval(cchk, Sc, o, Sc, fl)
         torch.cuda.synchronize()
         # the two contractions (integer digits / fp64) are compared within
         # themselves: they agree to ~1e-7, not bitwise
@@ -136,19 +157,19 @@ for rep in range(args.reps):
         ring = ring_bytes // (16 * N * N)
         out = out_flat[: ring * 4 * N * N].view(ring, 4, N, N)
         use(SF_EVAL_KERNEL_AUTO)
-        ctx.eval(coef, S, out, ring, base)  # untimed: re-warm after select()
+        run_eval(coef, S, out, ring, base)  # untimed: re-warm after select()
         for name, (kv, fl, opts) in variants.items():
             use(kv, opts)
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            ctx.eval(coef, S, out, ring, fl)
+            run_eval(coef, S, out, ring, fl)
             e1.record(stream)
             torch.cuda.synchronize()
             if rep:
                 res.setdefault((D, N, S, name), []).append(e0.elapsed_time(e1))
 for (D, N, S, name), v in res.items():
     ms = float(np.median(v))
-    gbs = S * (16 * N * N + 8 * D) / ms / 1e6
+    gbs = S * (16 * N * N + (24 if args.gain else 8) * D) / ms / 1e6
     print(f"D={D:2d} N={N} {name:10s}: median {ms:.3f} ms  min {min(v):.3f}  "
           f"{gbs:.1f} GB/s  frac {gbs / 8000:.3f}", flush=True)

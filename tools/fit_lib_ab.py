@@ -7,6 +7,13 @@ child process (SCREENFIT_LIB); the outputs go through .npy files under
 OUTDIR.
 
     python tools/fit_lib_ab.py OUTDIR LIB_A LIB_B [D:A:T:F ...] [--rounds 2]
+
+A LIB may carry library options, LIB@OPT=VALUE[,OPT=VALUE] (sf_set_option
+ids, e.g. lib.so@18=2: SF_OPT_FIT_SUBSET_DELETION 2), so one build can be
+A/B'd against itself.  A shape gain:D:A:T:F is the gain step's two fits as
+bench.py --screen gain runs them: the phase fit, then the XX / YY amplitude
+fit stacked along the station axis (niter 3, block sigma, no reference); its
+outputs compared are the amplitude fit's.
 """
 import json
 import os
@@ -18,17 +25,20 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def child(out, shape, keep):
+def child(out, shape, keep, opts):
     sys.path.insert(0, os.path.join(REPO, "ska-sdp-screen-fitting_amd"))
     import torch
     from ska_sdp_screen_fitting_amd import geometry, get_context
-    from ska_sdp_screen_fitting_amd._lib import library_identity
+    from ska_sdp_screen_fitting_amd._lib import SF_SCREEN_AMPLITUDE, library_identity
     from ska_sdp_screen_fitting_amd.stationscreen import station_orders
-    from ska_sdp_screen_fitting_amd.synthetic import make_solutions
+    from ska_sdp_screen_fitting_amd.synthetic import make_amplitudes, make_solutions
 
-    D, A, T, F = (int(v) for v in shape.split(":"))
+    gain = shape.startswith("gain:")
+    D, A, T, F = (int(v) for v in shape.split(":")[-4:])
     dev = torch.device("cuda", 0)
     ctx = get_context(0)
+    for k, v in opts:
+        ctx.set_option(k, v)
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)
     s = make_solutions(n_ant=A, n_time=T, n_freq=F, n_dir=D)
@@ -41,9 +51,25 @@ def child(out, shape, keep):
     order = torch.empty((T, F, A), dtype=torch.int32, device=dev)
     w_out = torch.empty_like(wt)
 
+    if gain:
+        make_amplitudes(s)
+        va = torch.from_numpy(np.ascontiguousarray(
+            np.concatenate([s.amp_val[..., p] for p in range(2)], axis=2))).to(dev)
+        wa = torch.from_numpy(np.ascontiguousarray(
+            np.concatenate([s.meta["amp_weight"][..., p] for p in range(2)], axis=2))).to(dev)
+        amp_order = min(12, max(3, int(np.round(D / 2))))
+        coef_a = torch.empty_like(va)
+        w_a = torch.empty_like(wa)
+        order_a = torch.empty((T, F, 2 * A), dtype=torch.int32, device=dev)
+
     def run():
         ctx.fit(ph, wt, T, F, A, st, ref_ant=0, coef=coef, order_out=order,
                 w_out=w_out, adjust_order=True, niter=2)
+        if gain:
+            ctx.fit(va, wa, T, F, 2 * A, [amp_order] * (2 * A),
+                    screen_type=SF_SCREEN_AMPLITUDE, niter=3, nsigma=5.0,
+                    adjust_order=True, ref_ant=-1, coef=coef_a, w_out=w_a,
+                    order_out=order_a)
 
     run()
     torch.cuda.synchronize()
@@ -57,12 +83,13 @@ def child(out, shape, keep):
         e1.synchronize()
         ms.append(e0.elapsed_time(e1))
     if keep:
-        np.save(out + "_order.npy", order.cpu().numpy())
-        np.save(out + "_w.npy", w_out.cpu().numpy())
-        np.save(out + "_coef.npy", coef.cpu().numpy())
+        o, w, c = (order_a, w_a, coef_a) if gain else (order, w_out, coef)
+        np.save(out + "_order.npy", o.cpu().numpy())
+        np.save(out + "_w.npy", w.cpu().numpy())
+        np.save(out + "_coef.npy", c.cpu().numpy())
     print(json.dumps({"shape": shape, "slots": T * F * A, "ms": float(np.median(ms)),
                       "ms_all": ms, "fit_stats": str(ctx.fit_stats()),
-                      "library": library_identity()["sha16"]}), flush=True)
+                      "library": library_identity()["sha16"], "opts": opts}), flush=True)
 
 
 def main():
@@ -76,15 +103,16 @@ def main():
     res = {"libs": libs, "runs": [], "compare": {}}
     for shape in shapes:
         tag = shape.replace(":", "_")
-        D, A, T, F = (int(v) for v in shape.split(":"))
+        D, A, T, F = (int(v) for v in shape.split(":")[-4:])
         small = T * F * A <= 2_000_000  # outputs compared (kept on disk) only then
         for rnd in range(rounds):
             for li, lib in enumerate(libs):
                 out = os.path.join(outdir, f"{tag}_{li}")
-                env = dict(os.environ, SCREENFIT_LIB=os.path.abspath(lib))
+                path, _, opts = lib.partition("@")
+                env = dict(os.environ, SCREENFIT_LIB=os.path.abspath(path))
                 keep = "1" if rnd == 0 and small else "0"
                 p = subprocess.run([sys.executable, "-u", __file__, "--child", out, shape,
-                                    keep], env=env, capture_output=True, text=True,
+                                    keep, opts], env=env, capture_output=True, text=True,
                                    timeout=600)
                 if p.returncode != 0:
                     print(p.stdout, p.stderr, file=sys.stderr)
@@ -118,6 +146,7 @@ def main():
 
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "--child":
-        child(sys.argv[2], sys.argv[3], sys.argv[4] == "1")
+        opts = [tuple(int(x) for x in kv.split("=")) for kv in sys.argv[5].split(",") if kv]
+        child(sys.argv[2], sys.argv[3], sys.argv[4] == "1", opts)
     else:
         main()
