@@ -1037,11 +1037,13 @@ def child_leg(extra, what, timeout_s=420, side=False, oracle=False):
         p = subprocess.run(cmd, env=env, capture_output=True, text=True,
                            timeout=timeout_s)
     except subprocess.TimeoutExpired:
-        return {"error": f"timed out after {timeout_s} s", "args": extra}
+        return {"error": f"timed out after {timeout_s} s", "args": extra,
+                "oracle_requested": oracle}
     wall = time.perf_counter() - t0
     # exit 3: the child's line is printed, its parity (oracle sample) failed
     if p.returncode not in (0, 3) or not p.stdout.strip():
-        return {"error": f"exit {p.returncode}: {p.stderr[-600:]}", "args": extra}
+        return {"error": f"exit {p.returncode}: {p.stderr[-600:]}", "args": extra,
+                "oracle_requested": oracle}
     r = json.loads(p.stdout.strip().splitlines()[-1])
     rf, chk = r["roofline"], r["check"]
     sm = chk.get("sampled_slots") or {}
@@ -1053,7 +1055,8 @@ def child_leg(extra, what, timeout_s=420, side=False, oracle=False):
         "kernel": rf["kernel"], "launch_ms": rf["launch_ms"],
         "bytes_per_launch": rf["bytes_per_launch"], "achieved_GBs": rf["achieved"],
         "frac": rf["frac"], "traffic": rf["traffic"], "mfma": r.get("mfma"),
-        "power": r.get("power"), "check": chk, "child_wall_s": wall, "what": what}
+        "power": r.get("power"), "check": chk, "child_wall_s": wall, "what": what,
+        "oracle_requested": oracle}
     if sm:
         out.update(sampled_slots=sm, checksums_match=sm.get("checksums_match"),
                    max_abs_err_vs_fp64=sm["max_abs_err_vs_fp64"], ok=sm["ok"])
@@ -1104,28 +1107,93 @@ def child_legs():
     }
 
 
-def rehearse_cpu(args, dist, world, rank, sol, setup, A, A_total, a0):
-    """--rehearse-cpu: the launcher and the gloo setup collectives without
-    a GPU -- every rank builds its shard and runs setup_shard; the line
-    reports each rank's shard and a digest of the setup it received (equal
-    on every rank).  No kernels run: ``value`` is null."""
+def child_leg_parity(side, line):
+    """Fold the child legs' oracle samples (their CPU baseline legs) into the
+    line's parity object; returns True when one failed.  A leg launched with
+    its oracle sample that errored, timed out or came back without the sample
+    counts as failed (its parity is unproven)."""
+    failed = False
+    for leg, key, pkey in (("config5", "oracle_check", "fit_oracle_sample_config5"),
+                           ("gain_config3", "oracle_check",
+                            "fit_oracle_sample_gain_config3"),
+                           ("gain_config3", "oracle_amp_check",
+                            "fit_oracle_amplitude_blocks_gain_config3"),
+                           ("tess_config3", "oracle_check",
+                            "tess_oracle_sample_config3")):
+        lr = side.get(leg)
+        if lr is None:
+            continue  # the leg did not run
+        c5 = lr.get(key)
+        if c5 is None:
+            if not lr.get("oracle_requested"):
+                continue
+            c5 = {"max_err": None, "tol": None, "ok": False, "slots": 0,
+                  "error": lr.get("error", f"no {key} in the leg's line")}
+        par = line.setdefault("parity", {})
+        par[pkey] = {"max_err": c5.get("max_err", c5.get("coef_max_abs_err")),
+                     "tol": c5["tol"], "ok": c5["ok"], "slots": c5["slots"]}
+        if "error" in c5:
+            par[pkey]["error"] = c5["error"]
+        if "all_ok" in par:
+            par["all_ok"] = par["all_ok"] and c5["ok"]
+        failed = failed or not c5["ok"]
+    return failed
+
+
+def setup_digest(setup):
+    """sha256 (16 hex digits) of the setup a rank works from: piercepoints,
+    grid coordinates, reference-station phases and index."""
     import hashlib
-    t0 = time.perf_counter()
-    if dist.is_initialized():
-        dist.barrier()
     h = hashlib.sha256()
     for a in (np.asarray(setup["piercepoints"]), np.asarray(setup["x"]),
               np.asarray(setup["y"]), setup["ref_phase"].cpu().numpy()):
         h.update(np.ascontiguousarray(a, np.float64).tobytes())
     h.update(str(setup["ref_ant"]).encode())
+    return h.hexdigest()[:16]
+
+
+def rehearse_cpu(args, dist, world, rank, sol, setup, A, A_total, a0,
+                 unsharded_setup=None):
+    """--rehearse-cpu: the launcher and the gloo setup collectives without
+    a GPU -- every rank builds its shard and runs setup_shard; the line
+    reports each rank's shard and a digest of the setup it received (equal
+    on every rank).  No kernels run: ``value`` is null.  Its ``parity``
+    object: every rank's setup equals the unsharded run's (rebuilt by rank
+    0, ``unsharded_setup``), the ranks' station orders concatenate to the
+    unsharded run's, and the rank identities pass the nccl one-card check
+    (check_distinct_devices, the refusal a real nccl job applies)."""
+    t0 = time.perf_counter()
+    if dist.is_initialized():
+        dist.barrier()
     T, F = sol.val.shape[:2]
     record = {"rank": rank, "ant": [a0, a0 + A], "slots": T * F * A,
-              "setup_sha16": h.hexdigest()[:16], "ref_ant": setup["ref_ant"],
+              "setup_sha16": setup_digest(setup), "ref_ant": setup["ref_ant"],
               "st_order": setup["st_order"]}
     dist_info = dist_block(args, world, record)
+    whole = unsharded_setup() if rank == 0 and unsharded_setup else None
     if dist.is_initialized():
         dist.barrier()
     if rank == 0:
+        from ska_sdp_screen_fitting_amd.distributed import check_distinct_devices
+        try:
+            check_distinct_devices(args.idents, "nccl")
+            nccl = {"ok": True}
+        except RuntimeError as exc:
+            nccl = {"ok": False, "error": str(exc)}
+        dist_info["nccl_distinct_check"] = nccl
+        parity = {"nccl_distinct_devices": nccl}
+        if whole is not None:
+            want = setup_digest(whole)
+            orders = sum((list(r["st_order"]) for r in dist_info["per_rank"]), [])
+            parity["shard_setup"] = {
+                "unsharded_setup_sha16": want,
+                "every_rank_equal": all(r["setup_sha16"] == want
+                                        for r in dist_info["per_rank"]),
+                "station_orders_equal": orders == list(whole["st_order"]),
+                "ranks": len(dist_info["per_rank"])}
+            parity["shard_setup"]["ok"] = (parity["shard_setup"]["every_rank_equal"]
+                                           and parity["shard_setup"]["station_orders_equal"])
+        parity["all_ok"] = all(v["ok"] for v in parity.values() if isinstance(v, dict))
         line = {"metric": METRIC, "value": None, "unit": "screen-slots/s",
                 "n_gpus": world, "steps": 0, "warmup": 0,
                 "ms_per_step": None, "higher_is_better": True,
@@ -1136,7 +1204,8 @@ def rehearse_cpu(args, dist, world, rank, sol, setup, A, A_total, a0):
                            "schedule": args.schedule},
                 "rehearsal": ("cpu: self-launch + gloo setup collectives only, "
                               "no kernels"),
-                "setup_s": time.perf_counter() - t0, "dist": dist_info}
+                "setup_s": time.perf_counter() - t0, "dist": dist_info,
+                "parity": parity}
         print(json.dumps(line), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
@@ -1424,7 +1493,18 @@ def main():
     log(f"shard ready: ant [{a0}, {a0 + A}) of {A_total}, {T * F * A} slots")
     if args.rehearse_cpu:
         args.schedule = pick_schedule(args, D, T)
-        return rehearse_cpu(args, dist, world, rank, sol, setup, A, A_total, a0)
+        # the setup the unsharded (N = 1) run computes, rebuilt by rank 0 on a
+        # one-rank group: the rehearsal's parity object compares every
+        # rank's received setup with it
+        solo = dist.new_group([0]) if dist.is_initialized() else None
+
+        def unsharded_setup():
+            whole = make_solutions(n_ant=A_total, n_time=T, n_freq=F, n_dir=D,
+                                   ant_offset=0, n_ant_total=A_total)
+            return setup_shard(whole, 0, A_total, FIELD_RA_DEG, FIELD_DEC_DEG,
+                               FIELD_WIDTH_DEG, cell, group=solo)
+        return rehearse_cpu(args, dist, world, rank, sol, setup, A, A_total, a0,
+                            unsharded_setup)
 
     ctx = get_context(gpu)
     if args.screen == "tess":
@@ -1859,22 +1939,8 @@ def main():
                         v["gpu_speedup"] = v["wall_s"] / fw[k]["wall_s"]
                 line["cpu_baseline"]["legs"] = legs
         # the child legs' own oracle samples (their CPU baseline legs)
-        for leg, key, pkey in (("config5", "oracle_check", "fit_oracle_sample_config5"),
-                               ("gain_config3", "oracle_check",
-                                "fit_oracle_sample_gain_config3"),
-                               ("gain_config3", "oracle_amp_check",
-                                "fit_oracle_amplitude_blocks_gain_config3"),
-                               ("tess_config3", "oracle_check",
-                                "tess_oracle_sample_config3")):
-            c5 = (side.get(leg) or {}).get(key)
-            if c5 is None:
-                continue
-            line.setdefault("parity", {})[pkey] = {
-                "max_err": c5.get("max_err", c5.get("coef_max_abs_err")),
-                "tol": c5["tol"], "ok": c5["ok"], "slots": c5["slots"]}
-            if "all_ok" in line["parity"]:
-                line["parity"]["all_ok"] = line["parity"]["all_ok"] and c5["ok"]
-            parity_failed = parity_failed or not c5["ok"]
+        if side:
+            parity_failed = child_leg_parity(side, line) or parity_failed
         line["library"] = dict(library_identity(), stale_counter_tables=dict(STALE_COUNTERS))
         print(json.dumps(line), flush=True)
     # release the CU-masked stream before the HIP runtime tears down

@@ -349,7 +349,30 @@ __device__ void fit_screen(const FitLds& L, const SubsetState& st, int D,
     }
   lds_sync();
   double screen;
-  if (screen_type == SF_SCREEN_PHASE) {
+  if (n == 2 && K == 1) {
+    // two unflagged directions: the reference's U_k = e_2 (see fit_once in
+    // kl_fit_fast.hip); v0..v2 were overwritten above, so the second
+    // direction's terms are gathered again
+    if (lp < D) {
+      v0[lp] = phi_d;
+      v1[lp] = w_d;
+    }
+    lds_sync();
+    const double w2 = v1[L.idx[1]];
+    const double ph2 = v0[L.idx[1]];
+    lds_sync();
+    const double iw = w2 > kPinvAtol ? 1.0 / w2 : 0.0;
+    double t_re, t_im = 0.0;
+    if (screen_type == SF_SCREEN_PHASE) {
+      double sn, cn;
+      sincos(ph2, &sn, &cn);
+      t_re = iw * (w2 * cn);
+      t_im = iw * (w2 * sn);
+    } else {
+      t_re = iw * (w2 * ph2);
+    }
+    screen = lp != 1 ? 0.0 : screen_type == SF_SCREEN_PHASE ? atan2(t_im, t_re) : t_re;
+  } else if (screen_type == SF_SCREEN_PHASE) {
     const double re = apply_pinv(L, st, ld, h1, v3);
     const double im = apply_pinv(L, st, ld, h2, v3);
     const double cre = apply_csub(L, n, ld, re, v3);

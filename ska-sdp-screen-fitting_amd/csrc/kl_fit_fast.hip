@@ -738,6 +738,23 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
     v2[l] = w_p;
   }
   lds_sync();
+  // Two unflagged directions (order clipped to n - 1 = 1): their C is
+  // [[0, b], [b, 0]], singular values |b| twice, and the reference's
+  // svd(C)[0] (LAPACK gesdd, stationscreen.py:427) is [[0, 1], [1, 0]] --
+  // unit vectors, not eigenvectors -- whose first column e_2 it keeps
+  // (:490-534): inv_u = pinv([w_2]) (0 below the 1e-3 cutoff), the fit
+  // C pinv(C) e_2 inv_u w_2 x_2 = (0, t), and the screen (0, atan2(t_im,
+  // t_re)) -- 0 = atan2(+0, +0) where the BLAS products leave +0
+  // (tests/golden/make_golden_ties.py pins it; LAPACK builds whose SVD
+  // leaves rounding residue there give atan2 of that residue instead)
+  const bool tie2 = n == 2 && K == 1;
+  double t_re = 0.0, t_im = 0.0;
+  if (tie2) {
+    const double w2 = v2[1];
+    const double iw = w2 > kAtol ? 1.0 / w2 : 0.0;
+    t_re = iw * v0[1];
+    t_im = iw * v1[1];
+  }
   double a1 = 0.0, a2 = 0.0;
   if (l < K) {
 #pragma unroll kMatVecUnroll
@@ -819,6 +836,8 @@ __device__ void fit_once(const FastLds& L, const Basis& B, int D, int ld,
       cim += u * v1[k];
     }
     screen = (screen_type == SF_SCREEN_PHASE) ? M::arctan2(cim, cre) : cre;
+    if (tie2)
+      screen = l != 1 ? 0.0 : (screen_type == SF_SCREEN_PHASE) ? M::arctan2(t_im, t_re) : t_re;
   }
   lds_sync();
   if (l < n) v2[l] = screen;

@@ -139,6 +139,51 @@ def test_schedule_is_the_same_at_every_world_size():
     s1, s8 = lines[1]["config"]["schedule"], lines[8]["config"]["schedule"]
     assert s1 == s8
     assert s1["coef_sets"] == 1 and s1["time_chunks"] == 1
+    # the N = 8 line: its parity object holds (every
+    # rank's setup = the unsharded run's, station orders concatenate to
+    # it, the rank identities pass the nccl one-card check), one per_rank
+    # entry per rank, eight distinct device identities
+    l8 = lines[8]
+    assert l8["parity"]["all_ok"] is True
+    assert l8["parity"]["shard_setup"]["ranks"] == 8
+    assert l8["parity"]["shard_setup"]["every_rank_equal"]
+    assert l8["parity"]["shard_setup"]["station_orders_equal"]
+    d = l8["dist"]
+    assert [r["rank"] for r in d["per_rank"]] == list(range(8))
+    assert len({dv["pci"] for dv in d["devices"]}) == 8 == d["distinct_devices"]
+    assert d["nccl_distinct_check"]["ok"] is True
+    assert lines[1]["parity"]["all_ok"] is True
+
+
+def test_child_leg_parity_fails_on_a_broken_leg():
+    """a child leg launched with its oracle sample that errored,
+    timed out or came back without the sample fails the line's parity
+    (bench.child_leg_parity); legs that passed, or did not run, do not."""
+    sys.path.insert(0, REPO)
+    import bench
+    ok = {"max_err": 1e-12, "tol": 1e-8, "ok": True, "slots": 128}
+    good = {"config5": {"oracle_requested": True, "oracle_check": dict(ok)},
+            "gain_config3": {"oracle_requested": True, "oracle_check": dict(ok),
+                             "oracle_amp_check": dict(ok, coef_max_abs_err=1e-13)},
+            "tess_config3": {"oracle_requested": True, "oracle_check": dict(ok)}}
+    line = {"parity": {"all_ok": True}}
+    assert bench.child_leg_parity(good, line) is False
+    assert line["parity"]["all_ok"] and len(line["parity"]) == 5
+    for broken in ({"error": "exit 134: abort", "oracle_requested": True},
+                   {"error": "timed out after 900 s", "oracle_requested": True},
+                   {"oracle_requested": True, "value": 1.0}):
+        side = dict(good, config5=broken)
+        line = {"parity": {"all_ok": True}}
+        assert bench.child_leg_parity(side, line) is True
+        assert line["parity"]["all_ok"] is False
+        assert line["parity"]["fit_oracle_sample_config5"]["ok"] is False
+    # a gain leg without its amplitude-block sample
+    side = dict(good, gain_config3={"oracle_requested": True, "oracle_check": dict(ok)})
+    line = {"parity": {"all_ok": True}}
+    assert bench.child_leg_parity(side, line) is True
+    # a leg that did not run is not a failure
+    line = {"parity": {"all_ok": True}}
+    assert bench.child_leg_parity({"config5": good["config5"]}, line) is False
 
 
 def test_pick_schedule_defaults():

@@ -863,20 +863,11 @@ def test_subset_deletion_edge_cases(ctx, dev, name, mode):
         return
     np.testing.assert_array_equal(dele[3], jac[3])
     np.testing.assert_array_equal(dele[2], jac[2])
-    # coefficients, except where the slot's subset basis has two eigenvalues
-    # of equal |lambda| (order between them undefined, the order-K truncation
-    # may keep either; the case above, only at D = 4 here)
-    tie = set()
-    for m, n, ej in zip(masks_j, ns, pool_j):
-        a = np.sort(np.abs(ej[D * D:D * D + n]))
-        if n > 1 and np.min(np.diff(a)) <= 1e-9 * lmax:
-            tie.add(int(m))
-    bits = (dele[2] > 0).astype(np.uint64) << np.arange(D, dtype=np.uint64)
-    slot_mask = bits.sum(axis=-1)
-    keep = ~np.isin(slot_mask, np.array(sorted(tie), dtype=np.uint64))
-    assert name == "d4" or not tie
+    # coefficients everywhere: the two-direction masks (d4), whose +-b
+    # eigenvalues either solver may order either way, fit on the reference's
+    # e_2 column (fit_once), not on the eigenvector order (round 6)
     scale = max(1.0, np.abs(jac[0]).max())
-    assert np.abs(dele[0] - jac[0])[keep].max() <= 1e-9 * scale
+    assert np.abs(dele[0] - jac[0]).max() <= 1e-9 * scale
 
 
 @pytest.mark.parametrize("name", ["heavy50", "lattice25", "d4", "synth20"])
@@ -962,3 +953,33 @@ def test_threads_fit_on_private_contexts(dev):
         t.join(timeout=300)
     assert not errors, errors
     assert all(v == 4 for v in done.values()), done
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+@pytest.mark.parametrize("name", ["ties4", "ties6"])
+def test_fit_vs_reference_golden_ties(ctx, dev, name, mode):
+    """The reference run with many two-direction slots
+    (tests/golden/make_golden_ties.py: D = 4 / 6, 40 % flags): its order-1
+    fit there keeps LAPACK's first U column e_2 of the tied 2 x 2 subset
+    (fit_once, kl_fit_fast.hip), under every subset-basis schedule (the
+    Jacobi, deletions from ancestors / the global basis / auto): orders and
+    flagged weights bit for bit, coefficients and residuals <= 1e-8 --
+    except the slots where the reference's own LAPACK left rounding residue
+    in that U (``tie_residue``, recorded by the generator: atan2 of the
+    residue)."""
+    from ska_sdp_screen_fitting_amd._lib import SF_OPT_FIT_SUBSET_DELETION
+    g = load_golden(name)
+    ctx.set_option(SF_OPT_FIT_SUBSET_DELETION, mode)
+    try:
+        coef, resid, w_out, orders = gpu_fit(ctx, dev, g)
+    finally:
+        ctx.set_option(SF_OPT_FIT_SUBSET_DELETION, 1)
+    np.testing.assert_array_equal(orders, g["orders"])
+    np.testing.assert_array_equal(w_out, g["w_out"])
+    keep = ~g["tie_residue"]
+    n2 = (g["w_out"] > 0).sum(axis=-1) == 2
+    assert (keep & n2).sum() >= 10
+    scale = max(1.0, np.abs(g["coef"]).max())
+    err = np.abs(coef - g["coef"]).max(axis=-1)
+    assert err[keep].max() <= 1e-8 * scale, np.argwhere(err > 1e-8 * scale)[:8]
+    assert np.abs(resid - g["resid"]).max(axis=-1)[keep].max() <= 1e-8

@@ -120,3 +120,28 @@ def test_patch_pixels_sin_projection():
                                   (-cell, cell))
         np.testing.assert_allclose(px, g[f"patch_pix{n}"][0], atol=1e-8)
         np.testing.assert_allclose(py, g[f"patch_pix{n}"][1], atol=1e-8)
+
+
+@pytest.mark.parametrize("name", ["ties4", "ties6"])
+def test_fit_matches_reference_ties(name):
+    """Slots with exactly two unflagged directions (tests/golden/
+    make_golden_ties.py, the reference run at D = 4 / 6 with 40 % flags):
+    the 2 x 2 subset C = [[0, b], [b, 0]] has |eigenvalues| |b| twice and
+    the reference's order-1 fit keeps the first column of LAPACK's U, e_2.
+    The oracle (numpy's LAPACK) reproduces the reference's orders, flags and
+    coefficients, except at the slots where the reference's LAPACK left
+    rounding residue in that U (``tie_residue``: its screen there is atan2
+    of the residue)."""
+    g = load_golden(name)
+    n2 = (g["w_out"] > 0).sum(axis=-1) == 2
+    assert n2.sum() >= 10
+    r = okl.run_phase(g["val"], g["weight"], g["ant_pos"], g["piercepoints"],
+                      int(g["ref_ant"]), int(g["order"]))
+    np.testing.assert_array_equal(r["orders"], g["orders"])
+    np.testing.assert_array_equal(r["w_out"], g["w_out"])
+    keep = ~g["tie_residue"]
+    err = np.abs(r["coef"] - g["coef"]).max(axis=-1)
+    scale = max(1.0, np.abs(g["coef"]).max())
+    assert np.nanmax(err[keep]) <= 1e-9 * scale
+    assert np.nanmax(np.abs(r["resid"] - g["resid"]).max(axis=-1)[keep]) <= 1e-9
+    assert np.all(err[keep & n2] <= 1e-9 * scale)

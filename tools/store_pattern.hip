@@ -22,6 +22,9 @@
 //   between store bursts, a barrier per group, LDS-capped occupancy)
 //   tools/store_pattern GiB 2 [R]   (2: long launches, R passes of the ring)
 //   tools/store_pattern GiB 3 [R]   (3: FMA "compute" vs sleep between bursts)
+//   tools/store_pattern GiB 4 [R]   (4, round 6: pitched rings -- the slot
+//                                    and plane pitches set off their powers
+//                                    of two by 4 KiB or 256 B)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -207,6 +210,62 @@ __global__ __launch_bounds__(64 * NW) void rows4_t(float* out, long P, long S, l
   }
 }
 
+// round 6: the register-tile and LDS-staged orders on a PITCHED ring: plane
+// q of ring slot r starts at r * sp + q * qp floats (the eval's layout has
+// qp = P, sp = 4 P: every concurrent store stream of the register tile sits
+// a power-of-two distance from the next -- 1 MiB at 256^2, 4 MiB at 512^2)
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void rows4p(float* out, long P, long S, long n_pb,
+                                                  long n_sc, int G, int lb, int xi,
+                                                  long ring, long qp, long sp) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  long pb, sc;
+  item(blockIdx.x, n_pb, n_sc, lb, xi, pb, sc);
+  if (sc >= n_sc) return;
+  const long p0 = (pb * NW + w) * 64 + (l & 15) * 4;
+  if (p0 >= P) return;
+  const v4f v = {1.f, 2.f, 3.f, (float)l};
+  for (int g = 0; g < G; ++g) {
+    const long s0 = (sc * G + g) * 16;
+    if (s0 >= S) return;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long s = s0 + (l >> 4) + 4 * r;
+      if (s < S) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) st(out + (s0 % ring + (s - s0)) * sp + q * qp + p0, v);
+      }
+    }
+  }
+}
+
+template <int NW, int RUN>
+__global__ __launch_bounds__(64 * NW) void contigp(float* out, long P, long S, long n_pb,
+                                                   long n_sc, int G, int xi, long ring,
+                                                   long qp, long sp) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  long pb, sc;
+  item(blockIdx.x, n_pb, n_sc, 0, xi, pb, sc);
+  if (sc >= n_sc) return;
+  const long pix0 = pb * RUN;
+  const v4f v = {1.f, 2.f, 3.f, (float)l};
+  for (int g = 0; g < G; ++g) {
+    const long s0 = (sc * G + g) * 16;
+    if (s0 >= S) return;
+    for (int j = 0; j < 16 / NW; ++j) {
+      const long s = s0 + w * (16 / NW) + j;
+      if (s >= S) continue;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int c = 0; c < RUN / 256; ++c) {
+          const long p = pix0 + c * 256 + 4 * l;
+          if (p < P) st(out + (s0 % ring + (s - s0)) * sp + q * qp + p, v);
+        }
+    }
+  }
+}
+
 int main(int argc, char** argv) {
   const long gib = argc > 1 ? atol(argv[1]) : 16;
   const long bytes = gib << 30;
@@ -298,6 +357,47 @@ int main(int argc, char** argv) {
         time(name, wrote, [&] {
           hipLaunchKernelGGL((contig_t<16, 1024>), dim3((unsigned)(n_pb * n_sc)), dim3(1024),
                              131584, 0, out, P, S, n_pb, n_sc, G, 1, sl, 1, ring);
+        });
+      }
+    }
+    (void)hipFree(out);
+    return 0;
+  }
+  if (argc > 2 && atoi(argv[2]) == 4) {
+    // round 6: address interleave.  The register tile's
+    // concurrent (slot, plane) streams sit power-of-two pitches apart; are
+    // non-power-of-two pitches faster?  Long launches (R passes of the ring)
+    const long R = argc > 3 ? atol(argv[3]) : 8;
+    for (long N : {256L, 512L}) {
+      const long P = N * N;
+      // (plane pad, slot pad) in floats: 0, 256 B, 4 KiB
+      const long pads[][2] = {{0, 0}, {0, 64}, {0, 1024}, {64, 0}, {1024, 0},
+                              {64, 64}, {1024, 1024}, {0, 16384}};
+      for (const auto& pd : pads) {
+        const long qp = P + pd[0], sp = 4 * qp + pd[1];
+        const long ring = (bytes / 4 / sp) / 16 * 16;
+        const long S = ring * R;
+        const long wrote = S * 16 * P;
+        // the register tile as the evaluations run it: 256^2 gain (64
+        // groups, contiguous map), 512^2 config 5 (4 groups, 8 bands,
+        // interleaved map)
+        const int G = N == 256 ? 64 : 4, lb = N == 256 ? 0 : 3, xi = N == 256 ? 0 : 1;
+        const long n_pb = P / 256;
+        const long n_sc = (S + 16 * G - 1) / (16 * G);
+        snprintf(name, sizeof name, "pitch rows4  %ld^2 g%-2d +%ldB plane +%ldB slot", N, G,
+                 pd[0] * 4, pd[1] * 4);
+        time(name, wrote, [&] {
+          hipLaunchKernelGGL(rows4p<4>, dim3((unsigned)(n_pb * n_sc)), dim3(256), 0, 0, out, P,
+                             S, n_pb, n_sc, G, lb, xi, ring, qp, sp);
+        });
+        // the LDS16 order (config 4: 4 KiB runs, 2 groups, interleaved map)
+        const int G2 = 2;
+        const long n_pb2 = P / 1024, n_sc2 = (S + 16 * G2 - 1) / (16 * G2);
+        snprintf(name, sizeof name, "pitch contig %ld^2 g%-2d +%ldB plane +%ldB slot", N, G2,
+                 pd[0] * 4, pd[1] * 4);
+        time(name, wrote, [&] {
+          hipLaunchKernelGGL((contigp<16, 1024>), dim3((unsigned)(n_pb2 * n_sc2)), dim3(1024), 0,
+                             0, out, P, S, n_pb2, n_sc2, G2, 1, ring, qp, sp);
         });
       }
     }
