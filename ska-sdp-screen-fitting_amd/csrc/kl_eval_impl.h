@@ -99,9 +99,15 @@ __device__ __forceinline__ void rev_reduce_n(float (&f)[N], const double (&rev)[
 constexpr double kRevMagic = 1572864.0;          // 1.5 * 2^20
 constexpr float kTwoM32 = 2.3283064365386963e-10f;  // 2^-32
 constexpr int kMagicMaxKS = 11;
-// gain screens on the LDS-staged kernels (round 6): up to this many k-steps,
-// and the shape the auto choice takes
-constexpr int kGainLdsMaxKS = 11;
+// gain screens on the LDS-staged kernels (round 6, "Tried" in DESIGN.md):
+// bit-equal to the register tile but slower (0.48-0.56 vs 0.66 of 8 TB/s),
+// so the shipped library compiles none (1.9 MB of code objects); a variant
+// build with -DSF_EVAL_GAIN_LDS=1 has them for kGainLdsMaxKS k-steps, where
+// SF_OPT_EVAL_KERNEL forces them (the auto choice stays on the tile)
+#ifndef SF_EVAL_GAIN_LDS
+#define SF_EVAL_GAIN_LDS 0
+#endif
+constexpr int kGainLdsMaxKS = SF_EVAL_GAIN_LDS ? 11 : 0;
 constexpr int kGainLdsAuto = SF_EVAL_KERNEL_TILE;
 
 template <int KS>

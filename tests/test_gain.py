@@ -279,9 +279,11 @@ def test_gain_eval_finite_groups_and_scrub(gain, fast):
 @pytest.mark.parametrize("n_dir,grid", [(20, 256), (7, 128), (24, 60), (3, 40),
                                         (44, 32), (50, 64)])
 def test_gain_eval_kernels_agree(n_dir, grid):
-    """Every gain evaluation kernel -- the register tile and the LDS-staged
-    shapes (round 6: LDS4 / LDS8 / LDS8H / LDS16H, LDS16 mapped to LDS16H)
-    -- writes the same bits as the register tile, with plain, non-temporal
+    """Every gain evaluation kernel -- the register tile and, in a library
+    built with -DSF_EVAL_GAIN_LDS=1 (round 6, "Tried" in DESIGN.md), the
+    LDS-staged shapes LDS4 / LDS8 / LDS8H / LDS16H (LDS16 mapped to LDS16H;
+    the shipped library maps every forced shape to the tile) -- writes the
+    same bits as the register tile, with plain, non-temporal
     and big-endian stores, walking workgroups, both XCD maps, short work
     items, and through sf_kl_eval_sums (equal per-slot checksums).  Ragged
     slot count (45: a partial 16-slot group), grids that are not a multiple
