@@ -118,3 +118,32 @@ def test_tess_cpu_baseline_leg_checks_labels_and_fill():
     oc = line["cpu_baseline"]["oracle_check"]
     assert oc["ok"] and oc["labels_differ"] == 0 and oc["max_ulp"] <= 1, oc
     assert line["parity"]["all_ok"] and line["parity"]["tess_oracle_sample"]["ok"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("workload", ["config3", "config5"])
+def test_full_size_workload_fit_and_eval_vs_oracle(workload):
+    """Configs 3 and 5 at their FULL per-GPU size (config 3: 64 ant x 100 t
+    x 16 f x 20 dir, KL 256^2; config 5: the 64-of-512-station shard, 4000 t
+    x 64 f x 50 dir = 16.4 M slots, KL 512^2, integer-digit contraction,
+    discard + checksum mode), one timed step each as the bench line runs
+    them: the GPU fit of the whole workload against the oracle's fits of the
+    CPU baseline's sampled slots (orders and flags bit-equal, coefficients
+    <= 1e-8), the sampled slots' evaluation against an fp64 restatement of
+    kl_screen.py:444-449 and their streamed checksums."""
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--workload", workload,
+           "--steps", "1", "--warmup", "0", "--no-side-legs", "--no-fits",
+           "--no-child-legs", "--no-parity", "--cpu-workers", "8", "--cpu-fit-slots", "16",
+           "--cpu-eval-slots", "2", "--no-cpu-reference-path"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    S = {"config3": 64 * 100 * 16, "config5": 64 * 4000 * 64}[workload]
+    assert line["config"]["slots_per_gpu"] == S
+    chk = line["cpu_baseline"]["oracle_check"]
+    assert chk["ok"] and chk["orders_differ"] == 0 and chk["slots"] >= 64, chk
+    s = line["check"]["sampled_slots"]
+    assert s["ok"], s
+    if workload == "config5":
+        assert s.get("checksums_match") is True
+        assert line["dtype"].startswith("i8-digit")
