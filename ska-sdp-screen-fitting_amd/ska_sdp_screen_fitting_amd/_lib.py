@@ -445,6 +445,9 @@ def get_context(device=0):
 
 
 _idle = {}
+# idle contexts kept per device (more are closed: a context keeps the device
+# scratch of the largest call it ran)
+_IDLE_MAX = 4
 
 
 @contextlib.contextmanager
@@ -466,4 +469,8 @@ def private_context(device=0):
         yield ctx
     finally:
         with _ctx_lock:
-            _idle[device].append(ctx)
+            keep = len(_idle[device]) < _IDLE_MAX
+            if keep:
+                _idle[device].append(ctx)
+        if not keep:
+            ctx.close()  # sf_destroy: hipFree waits for the device

@@ -277,11 +277,20 @@ class VoronoiScreen(Screen):
         ny, nx = self.data_rasertize_template.shape
         S, D = ph_dev.shape
         # the fill's scratch (table, smoothing buffers) is the context's: a
-        # context of its own per call
+        # context of its own per call.  The call returns with its kernels
+        # queued, so the context carries an event of its last fill: the next
+        # holder's stream waits for it before reusing the scratch (another
+        # thread's stream is not ordered after this one)
         with private_context(self.device) as ctx, torch.cuda.device(dev):
-            ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+            stream = torch.cuda.current_stream(dev)
+            busy = getattr(ctx, "tess_busy", None)
+            if busy is not None:
+                stream.wait_event(busy)
+            ctx.set_stream(stream.cuda_stream)
             ctx.tess_fill(lab, nx, ny, ph_dev, D, S, out_dev, amp_xx=amp_xx,
                           amp_yy=amp_yy, smooth_pix=smooth_pix, flags=flags)
+            ctx.tess_busy = torch.cuda.Event()
+            ctx.tess_busy.record(stream)
         return out_dev
 
     def _upload(self, a):

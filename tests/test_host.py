@@ -128,3 +128,48 @@ def test_wg_jacobi_pair_shares_cover_every_pair_once():
                 ke = min(kb + share, npairs)
                 owned.extend(range(kb, ke))
             assert sorted(owned) == list(range(npairs)), (nw, n)
+
+
+def test_private_context_pool(monkeypatch):
+    """_lib.private_context (round 6): a context is held by one block at a
+    time, reused once released, and at most _IDLE_MAX idle contexts per
+    device are kept (the rest closed) -- checked with a stand-in Context,
+    no GPU."""
+    import threading
+    from ska_sdp_screen_fitting_amd import _lib
+
+    made, closed = [], []
+
+    class Fake:
+        def __init__(self, device):
+            self.device = device
+            made.append(self)
+
+        def close(self):
+            closed.append(self)
+
+    monkeypatch.setattr(_lib, "Context", Fake)
+    monkeypatch.setattr(_lib, "_idle", {})
+    with _lib.private_context(3) as a:
+        with _lib.private_context(3) as b:
+            assert a is not b                      # held exclusively
+    with _lib.private_context(3) as c:
+        assert c in (a, b)                         # reused, not created
+    assert len(made) == 2
+    # many concurrent holders: at most _IDLE_MAX stay idle afterwards
+    n = _lib._IDLE_MAX + 3
+    barrier = threading.Barrier(n)
+    held = []
+
+    def hold():
+        with _lib.private_context(5) as ctx:
+            held.append(ctx)
+            barrier.wait()
+
+    ths = [threading.Thread(target=hold) for _ in range(n)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert len({id(x) for x in held}) == n
+    assert len(_lib._idle[5]) == _lib._IDLE_MAX and len(closed) == 3

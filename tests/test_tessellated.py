@@ -549,3 +549,60 @@ def test_make_aterm_image_one_direction_forces_tessellated(tmp_path):
         want = fn(ph)[..., None, None]
         np.testing.assert_allclose(cube[:, :, :, p], np.broadcast_to(want, cube[:, :, :, p].shape),
                                    rtol=0, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_tess_fill_threads_on_two_streams():
+    """VoronoiScreen.eval_device from two threads, each on its own stream
+    (round 6): every call takes a private context, and a context's table /
+    smoothing scratch is reused only after its previous fill's event, so
+    the interleaved fills equal the same fills run one at a time."""
+    import threading
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from ska_sdp_screen_fitting_amd.voronoi_screen import VoronoiScreen
+    g, radec = fixture_patches()
+    lab, _ = tessellation_template(radec, FIELD["rad"], FIELD["dec"], FIELD["width"],
+                                   0.05)
+    scr = VoronoiScreen.__new__(VoronoiScreen)
+    scr.data_rasertize_template = lab
+    scr.device = 0
+    scr._dev_cache = None
+    dev = torch.device("cuda", 0)
+    ref = int(g["ref_ant"])
+    ph_all = (g["val"] - g["val"][:, :, ref:ref + 1, :]).reshape(-1, 7)
+    n, S = 6, 96
+    ny, nx = lab.shape
+    phs = [torch.from_numpy(np.ascontiguousarray(ph_all[k * S:(k + 1) * S])).to(dev)
+           for k in range(2 * n)]
+    want = []
+    for p in phs:
+        o = torch.empty((S, 4, ny, nx), dtype=torch.float32, device=dev)
+        scr.eval_device(p, o, smooth_pix=0.5)
+        torch.cuda.synchronize()
+        want.append(o.cpu().numpy())
+    got = [None] * (2 * n)
+    errors = []
+
+    def worker(w):
+        try:
+            s = torch.cuda.Stream(dev)
+            with torch.cuda.stream(s):
+                for k in range(w, 2 * n, 2):
+                    o = torch.empty((S, 4, ny, nx), dtype=torch.float32, device=dev)
+                    scr.eval_device(phs[k], o, smooth_pix=0.5)
+                    got[k] = o
+            s.synchronize()
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    ths = [threading.Thread(target=worker, args=(w,)) for w in (0, 1)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=120)
+    assert not errors, errors
+    torch.cuda.synchronize()
+    for k in range(2 * n):
+        np.testing.assert_array_equal(got[k].cpu().numpy(), want[k])
