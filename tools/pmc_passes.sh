@@ -3,7 +3,7 @@
 # MI355X_MICROARCH.md "rocprofv3 PMC slots": <= 8 SQ, <= 4 TCC, <= 2 GRBM)
 # over one command; CSVs land in OUTDIR/<set>/.
 #   tools/pmc_passes.sh OUTDIR "SETS" -- python3 tools/eval_variants.py ...
-# SETS: any of occ mfma valu lds write fetch, and trace (a --kernel-trace
+# SETS: any of occ mfma valu lds write fetch ea, and trace (a --kernel-trace
 # --stats run: kernel durations without counter collection)
 set -e
 out=$1; sets=$2; shift 3
@@ -15,6 +15,9 @@ C[valu]="SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_IN
 C[lds]="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INST_CYCLES_VMEM_WR SQ_VMEM_WR_TA_DATA_FIFO_FULL SQ_VMEM_TA_CMD_FIFO_FULL SQ_VALU_MFMA_COEXEC_CYCLES SQ_INSTS_VALU_CVT SQ_INSTS_VALU_INT32 GRBM_GUI_ACTIVE"
 C[write]="WRITE_SIZE"
 C[fetch]="FETCH_SIZE"
+# round 6: the L2's memory-side write requests, their stalls (all DRAM
+# credit stalls on gfx950) and the queue level per cycle
+C[ea]="TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_STALL_sum TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum TCC_EA0_WRREQ_LEVEL_sum GRBM_GUI_ACTIVE"
 # the identity of the library these counters are taken on (bench.py reports
 # a table entry only when it matches the library it loaded)
 mkdir -p "$out"
