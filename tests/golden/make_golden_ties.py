@@ -86,6 +86,47 @@ def main():
             piercepoints=fit["piercepoints"], mid_ra=fit["mid_ra"],
             mid_dec=fit["mid_dec"], beta=fit["beta"], r_0=fit["r_0"],
             C=fit["C"], pinv_c=fit["pinv_c"], U=fit["U"], tie_residue=residue)
+    # tec screens (stationscreen.py:549-562: no atan2; the screen is C times
+    # the fit): the same two-direction rule, niter 3 (the block sigma of Q6)
+    s = mg.make_solutions(n_ant=6, n_time=8, n_freq=2, n_dir=4, seed=414,
+                          flag_frac=0.4, outlier_frac=0.02)
+    w = s.weight
+    for idx in np.argwhere((w > 0).sum(axis=-1) < 2):
+        slot = w[tuple(idx)]
+        for d in range(slot.size):
+            if (slot > 0).sum() >= 2:
+                break
+            if slot[d] <= 0:
+                slot[d] = 1.0
+    val = s.val * 0.05  # TECU-sized values
+    sol = dict(val=val, weight=w, times=s.times, freqs=s.freqs,
+               dir_names=s.dir_names, ant_names=s.ant_names,
+               dir_radec=s.dir_radec, ant_pos=s.ant_pos)
+
+    class TecSoltab(mg.DuckSoltab):
+        name = "tec000"
+
+        def get_type(self):
+            return "tec"
+
+    st = TecSoltab(sol)
+    ref = mg.reference_station(st.weight, 10)
+    rc = mg.stationscreen.run(st, "tec_screen000", order=3, niter=3, ref_ant=ref,
+                              scale_order=True, adjust_order=True, ncpu=1)
+    assert rc == 0
+    ss = st.get_solset()
+    scr, res = ss.made["tec_screen000"], ss.made["tec_screen000resid"]
+    w_out = scr.weights.astype(np.float32)
+    print("ties4tec ref", ref, "slots with 2 unflagged",
+          int(((w_out > 0).sum(-1) == 2).sum()))
+    np.savez_compressed(
+        os.path.join(HERE, "ties4tec.npz"),
+        val=val, weight=w, times=s.times, freqs=s.freqs,
+        dir_names=np.array(s.dir_names), ant_names=np.array(s.ant_names),
+        dir_radec=s.dir_radec, ant_pos=s.ant_pos, ref_ant=ref, order=3, niter=3,
+        coef=scr.vals, w_out=w_out, resid=res.vals,
+        orders=res.weights[..., 0].astype(np.int32),
+        piercepoints=ss.obj._v_file.arrays["/sol000/tec_screen000/piercepoint"])
     print("done")
 
 

@@ -80,3 +80,55 @@ def test_tec_fit_vs_reference(tec, case):
     torch.cuda.synchronize()
     _check(g, case, coef.cpu().numpy(), resid.cpu().numpy(), w_out.cpu().numpy(),
            orders.cpu().numpy(), 1e-8)
+
+
+def _ties():
+    g = load_golden("ties4tec")
+    return {"val": g["val"], "weight": g["weight"], "ant_pos": g["ant_pos"],
+            "piercepoints": g["piercepoints"], "order": g["order"], "niter": g["niter"],
+            "t_ref_ant": g["ref_ant"], "t_coef": g["coef"], "t_w_out": g["w_out"],
+            "t_resid": g["resid"], "t_orders": g["orders"]}
+
+
+def test_oracle_tec_ties_vs_reference():
+    """tests/golden/ties4tec.npz (make_golden_ties.py): the reference's tec
+    fit at D = 4 with 40 % flags -- 46 slots keep exactly two unflagged
+    directions, whose order-1 fit keeps LAPACK's first U column e_2 of the
+    tied 2 x 2 subset (no atan2 for tec: the screen there is C times the
+    fit, (0, t) to rounding)."""
+    g = _ties()
+    assert ((g["t_w_out"] > 0).sum(-1) == 2).sum() >= 20
+    r = okl.run_soltab(g["val"], g["weight"], g["ant_pos"], g["piercepoints"],
+                       int(g["t_ref_ant"]), int(g["order"]), "tec",
+                       niter=int(g["niter"]))
+    _check(g, "t", r["coef"], r["resid"], r["w_out"], r["orders"], 1e-10)
+
+
+@pytest.mark.gpu
+def test_tec_ties_fit_vs_reference():
+    """The GPU tec fit on the same two-direction-heavy reference run: orders
+    and flags bit-equal, coefficients / residuals <= 1e-8."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from ska_sdp_screen_fitting_amd import get_context
+    from ska_sdp_screen_fitting_amd._lib import SF_SCREEN_TEC
+    from ska_sdp_screen_fitting_amd.stationscreen import station_orders
+    g = _ties()
+    dev = torch.device("cuda", 0)
+    ctx = get_context(0)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    ctx.set_basis(g["piercepoints"])
+    ref = int(g["t_ref_ant"])
+    st = station_orders(g["ant_pos"], ref, int(g["order"]))
+    T, F, A, D = g["val"].shape
+    v = torch.from_numpy(np.ascontiguousarray(g["val"])).to(dev)
+    w = torch.from_numpy(np.ascontiguousarray(g["weight"])).to(dev)
+    coef, resid = torch.zeros_like(v), torch.zeros_like(v)
+    w_out = torch.empty_like(w)
+    orders = torch.zeros((T, F, A), dtype=torch.int32, device=dev)
+    ctx.fit(v, w, T, F, A, st, screen_type=SF_SCREEN_TEC, niter=int(g["niter"]),
+            ref_ant=ref, coef=coef, resid=resid, w_out=w_out, order_out=orders)
+    torch.cuda.synchronize()
+    _check(g, "t", coef.cpu().numpy(), resid.cpu().numpy(), w_out.cpu().numpy(),
+           orders.cpu().numpy(), 1e-8)
