@@ -11,7 +11,10 @@ and the order-1 fit (``_fit_screen``, stationscreen.py:490-534, the order
 clipped to n_unflagged - 1 = 1 at :685-686) keeps its first column.  These
 sets pin what the reference does there.
 
-Usage:  /opt/conda/bin/python3.9 tests/golden/make_golden_ties.py
+Usage:  /opt/conda/bin/python3.9 tests/golden/make_golden_ties.py [amp]
+(``amp``: only the amplitude set -- run it under ``timeout``: a slot the
+block flags leave with one unflagged direction kills the reference's worker
+and the run hangs, see below)
 """
 
 import os
@@ -25,7 +28,65 @@ sys.path.insert(0, HERE)
 import make_golden as mg  # noqa: E402  (shims + reference imports)
 
 
+def amplitude_case(seed=424):
+    """The amplitude fit as KLScreen.fit calls it (kl_screen.py:96-125: order
+    min(12, max(3, round(D / 2))) = 3, niter 3, no order scaling, ref_ant -1)
+    at D = 4 with 40 % of the weights zero: the block sigma (Q6) and the
+    two-direction rule on log10 amplitudes, both pols."""
+    from ska_sdp_screen_fitting_amd.synthetic import make_amplitudes
+    s = mg.make_solutions(n_ant=6, n_time=6, n_freq=2, n_dir=4, seed=seed)
+    make_amplitudes(s, seed=seed + 1, flag_frac=0.4, outlier_frac=0.0)
+    w = s.meta["amp_weight"]
+    for idx in np.argwhere((w > 0).sum(axis=-2) < 2):   # [t, f, a, pol]
+        t, f, a, p = idx
+        slot = w[t, f, a, :, p]
+        for d in range(slot.size):
+            if (slot > 0).sum() >= 2:
+                break
+            if slot[d] <= 0:
+                slot[d] = 1.0
+    sol = dict(val=s.val, weight=s.weight, times=s.times, freqs=s.freqs,
+               dir_names=s.dir_names, ant_names=s.ant_names,
+               dir_radec=s.dir_radec, ant_pos=s.ant_pos)
+
+    class AmpSoltab(mg.DuckSoltab):
+        name = "amplitude000"
+
+        def __init__(self, sol, amp, wt):
+            super().__init__(sol)
+            self.val = np.array(amp, dtype=np.float64)
+            self.weight = np.array(wt, dtype=np.float32)
+            self.pol = np.array(["XX", "YY"])
+
+        def get_type(self):
+            return "amplitude"
+
+        def get_axes_names(self):
+            return ["time", "freq", "ant", "dir", "pol"]
+
+    st = AmpSoltab(sol, s.amp_val, w)
+    rc = mg.stationscreen.run(st, "amplitude_screen000", order=3, niter=3,
+                              ref_ant=-1, scale_order=False, adjust_order=True,
+                              ncpu=1)
+    assert rc == 0
+    ss = st.get_solset()
+    scr, res = ss.made["amplitude_screen000"], ss.made["amplitude_screen000resid"]
+    w_out = scr.weights.astype(np.float32)
+    print("ties4amp slots x pols with 2 unflagged",
+          int(((w_out > 0).sum(-2) == 2).sum()))
+    np.savez_compressed(
+        os.path.join(HERE, "ties4amp.npz"),
+        amp_val=s.amp_val, amp_weight=w, dir_radec=s.dir_radec,
+        amp_order=3, amp_coef=scr.vals, amp_w_out=w_out, amp_resid=res.vals,
+        amp_orders=res.weights[..., 0, :].astype(np.int32),
+        piercepoints=ss.obj._v_file.arrays["/sol000/amplitude_screen000/piercepoint"])
+
+
 def main():
+    if sys.argv[1:] == ["amp"]:
+        amplitude_case()
+        print("done")
+        return
     cases = {
         # D = 4 / 6 with 40 % of the (slot, direction) weights zero: masks
         # with exactly two unflagged directions (the 2 x 2 tie), one (K = 0)

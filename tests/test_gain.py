@@ -477,3 +477,48 @@ def test_stacked_pol_fit_equals_per_pol(gain):
             for a, b in zip(single, stacked):
                 assert np.array_equal(a.view(np.uint8),
                                       np.ascontiguousarray(b[:, :, p * A:(p + 1) * A]).view(np.uint8))
+
+
+def test_oracle_amplitude_ties_vs_reference():
+    """tests/golden/ties4amp.npz (make_golden_ties.py amp): the reference's
+    amplitude fit as KLScreen.fit calls it at D = 4 with 40 % of the weights
+    zero -- 80 (slot, pol) fits with exactly two unflagged directions, whose
+    order-1 fit keeps LAPACK's e_2 column of the tied 2 x 2 subset."""
+    g = load_golden("ties4amp")
+    assert ((g["amp_w_out"] > 0).sum(axis=-2) == 2).sum() >= 40
+    r = okl.run_amplitude(g["amp_val"], g["amp_weight"], g["piercepoints"],
+                          int(g["amp_order"]))
+    np.testing.assert_array_equal(r["orders"], g["amp_orders"])
+    np.testing.assert_array_equal(r["w_out"], g["amp_w_out"])
+    np.testing.assert_allclose(r["coef"], g["amp_coef"], rtol=0, atol=1e-10)
+    np.testing.assert_allclose(r["resid"], g["amp_resid"], rtol=0, atol=1e-10)
+
+
+@pytest.mark.gpu
+def test_amplitude_ties_fit_vs_reference():
+    """The GPU amplitude fit (both pols stacked along the station axis in one
+    call, as stationscreen.run does) on the two-direction-heavy reference
+    run: orders and flags bit-equal, coefficients / residuals <= 1e-8."""
+    from ska_sdp_screen_fitting_amd._lib import SF_SCREEN_AMPLITUDE
+    torch, dev = _torch_dev()
+    ctx = _ctx(torch, dev)
+    g = load_golden("ties4amp")
+    ctx.set_basis(g["piercepoints"])
+    T, F, A, D, P = g["amp_val"].shape
+    order = int(g["amp_order"])
+    v = np.concatenate([g["amp_val"][..., p] for p in range(P)], axis=2)
+    w = np.concatenate([g["amp_weight"][..., p] for p in range(P)], axis=2)
+    vd = torch.from_numpy(np.ascontiguousarray(v)).to(dev)
+    wd = torch.from_numpy(np.ascontiguousarray(w)).to(dev)
+    coef, resid, w_out = torch.empty_like(vd), torch.empty_like(vd), torch.empty_like(wd)
+    orders = torch.empty((T, F, P * A), dtype=torch.int32, device=dev)
+    ctx.fit(vd, wd, T, F, P * A, [order] * (P * A), screen_type=SF_SCREEN_AMPLITUDE,
+            niter=3, ref_ant=-1, coef=coef, resid=resid, w_out=w_out, order_out=orders)
+    torch.cuda.synchronize()
+    c, r, wo, o = (x.cpu().numpy() for x in (coef, resid, w_out, orders))
+    for p in range(P):
+        sl = slice(p * A, (p + 1) * A)
+        np.testing.assert_array_equal(o[:, :, sl], g["amp_orders"][..., p])
+        np.testing.assert_array_equal(wo[:, :, sl], g["amp_w_out"][..., p])
+        np.testing.assert_allclose(c[:, :, sl], g["amp_coef"][..., p], rtol=0, atol=1e-8)
+        np.testing.assert_allclose(r[:, :, sl], g["amp_resid"][..., p], rtol=0, atol=1e-8)
