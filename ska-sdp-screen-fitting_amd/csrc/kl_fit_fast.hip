@@ -279,7 +279,7 @@ __global__ __launch_bounds__(64 * NW) void kl_subset_eig_kernel(
 //     directions, launches run level 1, 2, ... in order, and a mask starts
 //     from its nearest decomposed ancestor -- the mask with its lowest
 //     flagged directions unflagged, whose deletions are the first ones of
-//     its own (found in the mask table; decomposed by an earlier call, or by
+//     its own (found in the mask table; decomposed by an earlier pass, or by
 //     this call's lower levels without falling back) -- so a mask whose
 //     parent is in the pool costs one deletion instead of one per flagged
 //     direction.  level 0: every new mask from the global basis.  Either
